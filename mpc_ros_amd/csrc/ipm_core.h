@@ -1,0 +1,978 @@
+// mpc_ros_amd/csrc/ipm_core.h -- per-problem structured interior-point solver (one problem per lane).
+//
+// This is the solve that replaces CppAD::ipopt::solve inside MPC::Solve
+// (mpc_ros/src/mpc_planner.cpp:373-375).  It runs Ipopt 3.12.8's algorithm --
+// primal-dual barrier method with monotone mu, fraction-to-the-boundary, filter
+// line search and inertia correction (Waechter & Biegler 2006; the reference's
+// options, mpc_planner.cpp:356-368, leave every algorithmic option at its default) --
+// on the reference NLP in its reference variable layout, so that its iterates
+// follow the reference solver's path and land in the same local minimum of this
+// nonconvex problem.  What differs is the linear algebra: instead of a sparse
+// LDL^T (MUMPS) of the (nx+ng)-dim KKT matrix, every Newton system is solved by
+// a stage-wise Riccati recursion on its block-tridiagonal structure, and Ipopt's
+// inertia test (n positive, m negative eigenvalues) is replaced by the equivalent
+// test that every stage's reduced control Hessian is positive definite.
+//
+// Notation: stage k has state s_k = (x, y, th, v, cte, eth) (k < N) and control
+// u_k = (w, a) (k < N-1).  Constraint rows: c_0 = s_0 - state_init and
+// c_{k+1} = s_{k+1} - F(s_k, u_k) (FG_eval, mpc_planner.cpp:153-216).  Rate
+// penalties couple u_{k-1} and u_k, so the Riccati state is augmented with u_{k-1}
+// (8 states, 2 controls).  Multipliers are kept in "row form" yh_r = c_scale_r * y_r
+// (Ipopt's scaled multiplier times the row scale), so the Lagrangian Hessian
+// sum_r yh_r grad^2 c_r is independent of the scaling.
+//
+// Everything the oracle (oracle/ipm.c) does, this does in the same order with the
+// same constants; tests/ compare the two iterate for iterate.
+#ifndef MPCG_IPM_CORE_H
+#define MPCG_IPM_CORE_H
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MPCG_HD __host__ __device__ __forceinline__
+#else
+#define MPCG_HD inline
+#endif
+
+namespace mpcg {
+
+struct IpmParams {
+    int N;
+    double dt, ref_cte, ref_eth, ref_v;
+    double w_cte, w_eth, w_v, w_w, w_a, w_dw, w_da;
+    double max_w, max_a, bound;
+    double tol;                 // Ipopt tol (default 1e-8)
+    double bound_relax_factor;  // Ipopt default 1e-8
+    double mu_init;             // Ipopt default 0.1
+    int max_iter;               // Ipopt default 3000
+    int filter_cap;             // filter entries kept per problem
+};
+
+// Status numbering of CppAD::ipopt::solve_result::status_type
+// (mpc_ros/include/cppad/ipopt/solve_result.hpp:30-46).
+enum : int32_t {
+    IPM_SUCCESS = 1,
+    IPM_MAXITER = 2,
+    IPM_RESTORATION_FAILURE = 9,
+    IPM_ERROR_IN_STEP = 10,
+    IPM_INVALID_NUMBER = 11,
+};
+
+// Workspace layout of one problem; element e lives at ws[e * stride].
+struct IpmLayout {
+    int N;
+    static constexpr int STAGE = 80;  // per-stage Riccati record (75 used)
+    // record offsets
+    static constexpr int RK = 0, RKFF = 16, RP = 18, Rp = 54, RA = 62, RD = 69;
+    MPCG_HD int nx() const { return 8 * N - 2; }
+    MPCG_HD int ng() const { return 6 * N; }
+    MPCG_HD int W(int i) const { return i; }
+    MPCG_HD int ZL(int i) const { return nx() + i; }
+    MPCG_HD int ZU(int i) const { return 2 * nx() + i; }
+    MPCG_HD int DW(int i) const { return 3 * nx() + i; }
+    MPCG_HD int Y(int r) const { return 4 * nx() + r; }
+    MPCG_HD int YP(int r) const { return 4 * nx() + ng() + r; }
+    MPCG_HD int ST(int k, int j) const { return 4 * nx() + 2 * ng() + STAGE * k + j; }
+    MPCG_HD int FI(int j) const { return 4 * nx() + 2 * ng() + STAGE * N + j; }
+    MPCG_HD int total(int cap) const { return 4 * nx() + 2 * ng() + STAGE * N + 2 * cap; }
+    // reference layout (mpc_planner.cpp:252-259)
+    MPCG_HD int vs(int s, int k) const { return s * N + k; }
+    MPCG_HD int vu(int j, int k) const { return 6 * N + j * (N - 1) + k; }
+    MPCG_HD int row(int s, int k) const { return s * N + k; }
+};
+
+template <typename T>
+struct IpmProblem {
+    T init[6];  // x, y, theta, v, cte, etheta (MPC::Solve state argument)
+    T c[4];     // reference polynomial coefficients
+};
+
+struct IpmResult {
+    int32_t status;
+    int32_t iters;
+    double obj;
+    double kkt_inf;
+};
+
+template <typename T>
+MPCG_HD void sc_t(T a, T* s, T* c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincos(a, s, c);
+#else
+    *s = sin(a);
+    *c = cos(a);
+#endif
+}
+
+template <typename T>
+MPCG_HD T tmax(T a, T b) { return a > b ? a : b; }
+template <typename T>
+MPCG_HD T tmin(T a, T b) { return a < b ? a : b; }
+
+// Sum of logs accumulated as mantissa * 2^exponent: one log per pass.
+template <typename T>
+struct LogAcc {
+    T m;
+    int e;
+    MPCG_HD void init() { m = 1; e = 0; }
+    MPCG_HD void mul(T v) {
+        int ex;
+        m = frexp(m * v, &ex);
+        e += ex;
+    }
+    MPCG_HD T value() const { return log(m) + (T)e * (T)0.69314718055994530942; }
+};
+
+// Linearisation of the dynamics of one stage at (s, u).
+template <typename T>
+struct Lin {
+    T st, ct, se, ce;  // sin/cos theta, sin/cos etheta
+    T f, f1, f2;       // f(x), f'(x), f''(x)
+    MPCG_HD void eval(const T* c, const T* s) {
+        sc_t(s[2], &st, &ct);
+        sc_t(s[5], &se, &ce);
+        const T x = s[0];
+        // f(x) = sum_k c_k x^k with CppAD::pow(x,k) = repeated products (pow_int.hpp:115-137)
+        f = c[0] + c[1] * x + c[2] * (x * x) + c[3] * (x * x * x);
+        f1 = c[1] + (T)2 * c[2] * x + (T)3 * c[3] * x * x;
+        f2 = (T)2 * c[2] + (T)6 * c[3] * x;
+    }
+    // F(s, u)   (mpc_planner.cpp:202-215)
+    MPCG_HD void next(const T* s, const T* u, T dt, T* out) const {
+        out[0] = s[0] + s[3] * ct * dt;
+        out[1] = s[1] + s[3] * st * dt;
+        out[2] = s[2] + u[0] * dt;
+        out[3] = s[3] + u[1] * dt;
+        out[4] = (f - s[1]) + s[3] * se * dt;
+        out[5] = s[5] + u[0] * dt;
+    }
+    // non-trivial entries of A = dF/ds (dF_c/dy = -1 and the unit diagonal are implicit)
+    MPCG_HD void jac(const T* s, T dt, T* a) const {
+        a[0] = -s[3] * st * dt;  // dx+/dth
+        a[1] = ct * dt;          // dx+/dv
+        a[2] = s[3] * ct * dt;   // dy+/dth
+        a[3] = st * dt;          // dy+/dv
+        a[4] = f1;               // dc+/dx
+        a[5] = se * dt;          // dc+/dv
+        a[6] = s[3] * ce * dt;   // dc+/deth
+    }
+};
+
+// y = A^T lam (6x6 dynamics Jacobian)
+template <typename T>
+MPCG_HD void AT_mul(const T* a, const T* lam, T* y) {
+    y[0] = lam[0] + a[4] * lam[4];
+    y[1] = lam[1] - lam[4];
+    y[2] = a[0] * lam[0] + a[2] * lam[1] + lam[2];
+    y[3] = a[1] * lam[0] + a[3] * lam[1] + lam[3] + a[5] * lam[4];
+    y[4] = 0;
+    y[5] = a[6] * lam[4] + lam[5];
+}
+// y = A x
+template <typename T>
+MPCG_HD void A_mul(const T* a, const T* x, T* y) {
+    y[0] = x[0] + a[0] * x[2] + a[1] * x[3];
+    y[1] = x[1] + a[2] * x[2] + a[3] * x[3];
+    y[2] = x[2];
+    y[3] = x[3];
+    y[4] = a[4] * x[0] - x[1] + a[5] * x[3] + a[6] * x[5];
+    y[5] = x[5];
+}
+
+MPCG_HD constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+template <typename T, class WS>
+struct IpmSolver {
+    const IpmParams& P;
+    const IpmProblem<T>& pr;
+    WS& ws;
+    IpmLayout L;
+    int N;
+    T dt;
+    T sl, su, wl, wu, al, au;        // relaxed bounds: states, angvel, accel
+    T sl0, su0, wl0, wu0, al0, au0;  // original bounds
+    T sf;                            // objective scale
+    T rs0[6], rs1[6];                // row scales: dynamics rows into stage 1 / into stages >= 2
+    T mu, tau;
+    // statistics of the current iterate (pass A)
+    T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
+    int nfilter;
+
+    MPCG_HD IpmSolver(const IpmParams& P_, const IpmProblem<T>& pr_, WS& ws_)
+        : P(P_), pr(pr_), ws(ws_), L{P_.N}, N(P_.N), dt((T)P_.dt) {}
+
+    MPCG_HD T rowscale(int s, int k) const { return k == 0 ? (T)1 : (k == 1 ? rs0[s] : rs1[s]); }
+    MPCG_HD T clo(int j) const { return j == 0 ? wl : al; }
+    MPCG_HD T chi(int j) const { return j == 0 ? wu : au; }
+
+    MPCG_HD void load_s(int k, T* s) const {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) s[j] = ws[L.W(L.vs(j, k))];
+    }
+    MPCG_HD void load_u(int k, T* u) const {
+        u[0] = ws[L.W(L.vu(0, k))];
+        u[1] = ws[L.W(L.vu(1, k))];
+    }
+
+    // objective pieces (unscaled) -- FG_eval cost, mpc_planner.cpp:122-147
+    MPCG_HD T cost_state(const T* s) const {
+        const T e1 = s[4] - (T)P.ref_cte, e2 = s[5] - (T)P.ref_eth, e3 = s[3] - (T)P.ref_v;
+        return (T)P.w_cte * e1 * e1 + (T)P.w_eth * e2 * e2 + (T)P.w_v * e3 * e3;
+    }
+    MPCG_HD void grad_state(const T* s, T* g) const {
+        g[0] = 0; g[1] = 0; g[2] = 0;
+        g[3] = (T)(2.0 * P.w_v) * (s[3] - (T)P.ref_v);
+        g[4] = (T)(2.0 * P.w_cte) * (s[4] - (T)P.ref_cte);
+        g[5] = (T)(2.0 * P.w_eth) * (s[5] - (T)P.ref_eth);
+    }
+    // gradient w.r.t. u_k given u_{k-1} (valid if k>=1) and u_{k+1} (valid if k<=N-3)
+    MPCG_HD void grad_ctrl(int k, const T* um, const T* u, const T* up, T* g) const {
+        g[0] = (T)(2.0 * P.w_w) * u[0];
+        g[1] = (T)(2.0 * P.w_a) * u[1];
+        if (k >= 1) {
+            g[0] += (T)(2.0 * P.w_dw) * (u[0] - um[0]);
+            g[1] += (T)(2.0 * P.w_da) * (u[1] - um[1]);
+        }
+        if (k <= N - 3) {
+            g[0] -= (T)(2.0 * P.w_dw) * (up[0] - u[0]);
+            g[1] -= (T)(2.0 * P.w_da) * (up[1] - u[1]);
+        }
+    }
+    MPCG_HD T hess_ctrl(int k, int j) const {
+        const double wd = j == 0 ? P.w_dw : P.w_da;
+        const double w = j == 0 ? P.w_w : P.w_a;
+        return (T)(2.0 * w + 2.0 * wd * ((k >= 1 ? 1 : 0) + (k <= N - 3 ? 1 : 0)));
+    }
+
+    // ------------------------------------------------------------------ setup
+    // Bounds of MPC::Solve (mpc_planner.cpp:303-325) relaxed as Ipopt does;
+    // gradient-based scaling at the user's starting point; starting point pushed
+    // inside the box; bound multipliers 1; least-squares equality multipliers.
+    MPCG_HD void rowscales_at(const T* s, const T* u, T* rs) const {
+        Lin<T> ln;
+        ln.eval(pr.c, s);
+        (void)u;
+        T m[6];
+        m[0] = tmax((T)1, tmax(fabs(s[3] * ln.st * dt), fabs(ln.ct * dt)));
+        m[1] = tmax((T)1, tmax(fabs(s[3] * ln.ct * dt), fabs(ln.st * dt)));
+        m[2] = tmax((T)1, dt);
+        m[3] = tmax((T)1, dt);
+        m[4] = tmax(tmax((T)1, fabs(ln.f1)), tmax(fabs(ln.se * dt), fabs(s[3] * ln.ce * dt)));
+        m[5] = tmax((T)1, dt);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) rs[j] = m[j] > (T)100 ? (T)100 / m[j] : (T)1;
+    }
+
+    MPCG_HD void setup() {
+        const T rl = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.bound));
+        sl0 = (T)-P.bound; su0 = (T)P.bound; sl = sl0 - rl; su = su0 + rl;
+        const T rw = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_w));
+        wl0 = (T)-P.max_w; wu0 = (T)P.max_w; wl = wl0 - rw; wu = wu0 + rw;
+        const T ra = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_a));
+        al0 = (T)-P.max_a; au0 = (T)P.max_a; al = al0 - ra; au = au0 + ra;
+        // objective scale from grad f at the user start (zeros except s_0)
+        T g[6];
+        grad_state(pr.init, g);
+        T gm = tmax(fabs(g[3]), tmax(fabs(g[4]), fabs(g[5])));
+        if (N >= 2) {
+            const T z[6] = {0, 0, 0, 0, 0, 0};
+            grad_state(z, g);
+            gm = tmax(gm, tmax(fabs(g[3]), tmax(fabs(g[4]), fabs(g[5]))));
+        }
+        sf = gm > (T)100 ? (T)100 / gm : (T)1;
+        const T u0[2] = {0, 0};
+        rowscales_at(pr.init, u0, rs0);
+        const T z6[6] = {0, 0, 0, 0, 0, 0};
+        rowscales_at(z6, u0, rs1);
+    }
+
+    MPCG_HD T push(T v, T lo, T hi) const {
+        const T pl = tmin((T)0.01 * tmax((T)1, (T)fabs(lo)), (T)0.01 * (hi - lo));
+        const T pu = tmin((T)0.01 * tmax((T)1, (T)fabs(hi)), (T)0.01 * (hi - lo));
+        if (v < lo + pl) v = lo + pl;
+        if (v > hi - pu) v = hi - pu;
+        return v;
+    }
+
+    MPCG_HD void init_point() {
+        for (int k = 0; k < N; ++k)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int i = L.vs(j, k);
+                ws[L.W(i)] = push(k == 0 ? pr.init[j] : (T)0, sl, su);
+                ws[L.ZL(i)] = 1;
+                ws[L.ZU(i)] = 1;
+            }
+        for (int k = 0; k < N - 1; ++k)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int i = L.vu(j, k);
+                ws[L.W(i)] = push((T)0, clo(j), chi(j));
+                ws[L.ZL(i)] = 1;
+                ws[L.ZU(i)] = 1;
+            }
+    }
+
+    // ---------------------------------------------------------------- pass A
+    // Statistics of the current iterate: objective, barrier log-sum, constraint
+    // violation (l1 and max), dual infeasibility, complementarity extrema, l1 norms.
+    MPCG_HD void stats() {
+        fval = 0; theta = 0; prim_inf = 0; prim_uns = 0; dual_inf = 0; compl0 = 0;
+        pmin = (T)INFINITY; pmax = -(T)INFINITY; l1y = 0; l1z = 0;
+        LogAcc<T> la;
+        la.init();
+        T Fprev[6], um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
+        if (N >= 2) load_u(0, u);
+        for (int k = 0; k < N; ++k) {
+            T s[6];
+            load_s(k, s);
+            const bool hasu = k < N - 1;
+            if (k + 1 < N - 1) load_u(k + 1, up);
+            // residual rows (s, k)
+            T yk[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? s[j] - pr.init[j] : s[j] - Fprev[j];
+                const T rsc = rowscale(j, k);
+                const T cs = rsc * c;
+                theta += fabs(cs);
+                prim_inf = tmax(prim_inf, (T)fabs(cs));
+                prim_uns = tmax(prim_uns, (T)fabs(c));
+                yk[j] = ws[L.Y(L.row(j, k))];
+                l1y += fabs(yk[j]) / rsc;
+            }
+            fval += cost_state(s);
+            // dual residual of the states
+            T g[6], at[6] = {0, 0, 0, 0, 0, 0};
+            grad_state(s, g);
+            Lin<T> ln;
+            T a[7];
+            T ynext[6];
+            if (hasu) {
+                ln.eval(pr.c, s);
+                ln.jac(s, dt, a);
+                ln.next(s, u, dt, Fprev);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) ynext[j] = ws[L.Y(L.row(j, k + 1))];
+                AT_mul(a, ynext, at);
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int i = L.vs(j, k);
+                const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+                const T rd = sf * g[j] - zl + zu + yk[j] - at[j];
+                dual_inf = tmax(dual_inf, (T)fabs(rd));
+                const T dl = w - sl, du = su - w;
+                la.mul(dl);
+                la.mul(du);
+                const T p1 = dl * zl, p2 = du * zu;
+                compl0 = tmax(compl0, tmax((T)fabs(p1), (T)fabs(p2)));
+                pmin = tmin(pmin, tmin(p1, p2));
+                pmax = tmax(pmax, tmax(p1, p2));
+                l1z += fabs(zl) + fabs(zu);
+            }
+            if (hasu) {
+                T gu[2];
+                grad_ctrl(k, um, u, up, gu);
+                fval += (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
+                if (k <= N - 3)
+                    fval += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
+                const T btw = dt * (ynext[2] + ynext[5]), bta = dt * ynext[3];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int i = L.vu(j, k);
+                    const T w = u[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+                    const T rd = sf * gu[j] - zl + zu - (j == 0 ? btw : bta);
+                    dual_inf = tmax(dual_inf, (T)fabs(rd));
+                    const T dl = w - clo(j), du = chi(j) - w;
+                    la.mul(dl);
+                    la.mul(du);
+                    const T p1 = dl * zl, p2 = du * zu;
+                    compl0 = tmax(compl0, tmax((T)fabs(p1), (T)fabs(p2)));
+                    pmin = tmin(pmin, tmin(p1, p2));
+                    pmax = tmax(pmax, tmax(p1, p2));
+                    l1z += fabs(zl) + fabs(zu);
+                }
+                um[0] = u[0]; um[1] = u[1];
+                u[0] = up[0]; u[1] = up[1];
+            }
+        }
+        logsum = la.value();
+    }
+
+    // ------------------------------------------------------- Riccati backward
+    // mode 0: Newton system of the barrier problem (Hessian of the Lagrangian + Sigma + delta_w I)
+    // mode 1: least-squares multiplier system (identity Hessian, zero constraint residual)
+    // Returns false when a stage's reduced control Hessian is not positive definite.
+    MPCG_HD bool riccati(int mode, T delta_w) {
+        T Pm[36], pv[8];
+        // terminal stage
+        {
+            const int k = N - 1;
+            T s[6];
+            load_s(k, s);
+            T g[6];
+            grad_state(s, g);
+#pragma unroll
+            for (int i = 0; i < 36; ++i) Pm[i] = 0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int i = L.vs(j, k);
+                const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+                if (mode == 0) {
+                    const T dl = w - sl, du = su - w;
+                    const T hd = (j >= 3 ? sf * (T)(2.0 * (j == 3 ? P.w_v : (j == 4 ? P.w_cte : P.w_eth))) : (T)0);
+                    Pm[pidx(j, j)] = hd + zl / dl + zu / du + delta_w;
+                    pv[j] = sf * g[j] - mu / dl + mu / du;
+                } else {
+                    Pm[pidx(j, j)] = 1;
+                    pv[j] = sf * g[j] - zl + zu;
+                }
+            }
+            pv[6] = 0; pv[7] = 0;
+#pragma unroll
+            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pm[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pv[i];
+        }
+        T up[2] = {0, 0};
+        if (N >= 2) load_u(N - 2, up);  // u_{k} for k = N-2 at loop start
+        T unext[2] = {0, 0};
+        for (int k = N - 2; k >= 0; --k) {
+            T s[6], u[2], um[2] = {0, 0}, snext[6];
+            load_s(k, s);
+            u[0] = up[0]; u[1] = up[1];
+            if (k >= 1) load_u(k - 1, um);
+            load_s(k + 1, snext);
+            Lin<T> ln;
+            ln.eval(pr.c, s);
+            T a[7];
+            ln.jac(s, dt, a);
+            T Fk[6];
+            ln.next(s, u, dt, Fk);
+            T d[6];
+            T yn[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                d[j] = (mode == 0) ? Fk[j] - snext[j] : (T)0;
+                yn[j] = ws[L.Y(L.row(j, k + 1))];
+            }
+            // stage Hessian Q (6x6, packed), R diag, coupling C, gradients q, r
+            T Q[21];
+#pragma unroll
+            for (int i = 0; i < 21; ++i) Q[i] = 0;
+            T q[6], r[2], R0, R1, C0 = 0, C1 = 0;
+            T g[6];
+            grad_state(s, g);
+            T gu[2];
+            grad_ctrl(k, um, u, unext, gu);
+            if (mode == 0) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const int i = L.vs(j, k);
+                    const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+                    const T dl = w - sl, du = su - w;
+                    const T hd = (j >= 3 ? sf * (T)(2.0 * (j == 3 ? P.w_v : (j == 4 ? P.w_cte : P.w_eth))) : (T)0);
+                    Q[pidx(j, j)] = hd + zl / dl + zu / du + delta_w;
+                    q[j] = sf * g[j] - mu / dl + mu / du;
+                }
+                // constraint curvature, weighted by the row-form multipliers of rows k+1
+                const T v = s[3];
+                Q[pidx(2, 2)] += yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;
+                Q[pidx(3, 2)] += yn[0] * ln.st * dt - yn[1] * ln.ct * dt;
+                Q[pidx(0, 0)] += -yn[4] * ln.f2;
+                Q[pidx(5, 5)] += yn[4] * v * ln.se * dt;
+                Q[pidx(5, 3)] += -yn[4] * ln.ce * dt;
+                T Rr[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int i = L.vu(j, k);
+                    const T w = u[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+                    const T dl = w - clo(j), du = chi(j) - w;
+                    Rr[j] = sf * hess_ctrl(k, j) + zl / dl + zu / du + delta_w;
+                    r[j] = sf * gu[j] - mu / dl + mu / du;
+                }
+                R0 = Rr[0]; R1 = Rr[1];
+                if (k >= 1) {
+                    C0 = -sf * (T)(2.0 * P.w_dw);
+                    C1 = -sf * (T)(2.0 * P.w_da);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const int i = L.vs(j, k);
+                    Q[pidx(j, j)] = 1;
+                    q[j] = sf * g[j] - ws[L.ZL(i)] + ws[L.ZU(i)];
+                }
+                R0 = 1; R1 = 1;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int i = L.vu(j, k);
+                    r[j] = sf * gu[j] - ws[L.ZL(i)] + ws[L.ZU(i)];
+                }
+            }
+            // PA = P' A_hat : nonzero columns 0,1,2,3,5 (rows 0..7)
+            T PA[8][5];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const T p0 = Pm[pidx(i, 0)], p1 = Pm[pidx(i, 1)], p2 = Pm[pidx(i, 2)];
+                const T p3 = Pm[pidx(i, 3)], p4 = Pm[pidx(i, 4)], p5 = Pm[pidx(i, 5)];
+                PA[i][0] = p0 + a[4] * p4;
+                PA[i][1] = p1 - p4;
+                PA[i][2] = a[0] * p0 + a[2] * p1 + p2;
+                PA[i][3] = a[1] * p0 + a[3] * p1 + p3 + a[5] * p4;
+                PA[i][4] = a[6] * p4 + p5;  // column 5 (eth)
+            }
+            // PB = P' B_hat (B_hat: w -> dt e2 + dt e5 + e6 ; a -> dt e3 + e7)
+            T PB[8][2];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                PB[i][0] = dt * (Pm[pidx(i, 2)] + Pm[pidx(i, 5)]) + Pm[pidx(i, 6)];
+                PB[i][1] = dt * Pm[pidx(i, 3)] + Pm[pidx(i, 7)];
+            }
+            // h = P' d_hat + p'
+            T h[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                T acc = pv[i];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) acc += Pm[pidx(i, j)] * d[j];
+                h[i] = acc;
+            }
+            const T Rt00 = R0 + dt * (PB[2][0] + PB[5][0]) + PB[6][0];
+            const T Rt01 = dt * (PB[2][1] + PB[5][1]) + PB[6][1];
+            const T Rt11 = R1 + dt * PB[3][1] + PB[7][1];
+            const T det = Rt00 * Rt11 - Rt01 * Rt01;
+            if (!(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11)) return false;
+            // S_tilde (2 x 8): columns 0,1,2,3,5 from B^T P A ; 6,7 coupling ; 4 zero
+            T St[2][8];
+            const int cm[5] = {0, 1, 2, 3, 5};
+#pragma unroll
+            for (int c = 0; c < 5; ++c) {
+                St[0][cm[c]] = dt * (PA[2][c] + PA[5][c]) + PA[6][c];
+                St[1][cm[c]] = dt * PA[3][c] + PA[7][c];
+            }
+            St[0][4] = 0; St[1][4] = 0;
+            St[0][6] = C0; St[0][7] = 0;
+            St[1][6] = 0;  St[1][7] = C1;
+            const T rt0 = r[0] + dt * (h[2] + h[5]) + h[6];
+            const T rt1 = r[1] + dt * h[3] + h[7];
+            const T i00 = Rt11 / det, i01 = -Rt01 / det, i11 = Rt00 / det;
+            T K[2][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                K[0][j] = -(i00 * St[0][j] + i01 * St[1][j]);
+                K[1][j] = -(i01 * St[0][j] + i11 * St[1][j]);
+            }
+            const T kf0 = -(i00 * rt0 + i01 * rt1);
+            const T kf1 = -(i01 * rt0 + i11 * rt1);
+            // P_new = Q_hat + A^T P A + St^T K ; p_new = q_hat + A^T h + St^T kff
+            T AtPA[8][8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                // column c of (P A) in full 8-col indexing
+                T col[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    col[i] = (c == 4 || c >= 6) ? (T)0 : PA[i][c == 5 ? 4 : c];
+                }
+                AtPA[0][c] = col[0] + a[4] * col[4];
+                AtPA[1][c] = col[1] - col[4];
+                AtPA[2][c] = a[0] * col[0] + a[2] * col[1] + col[2];
+                AtPA[3][c] = a[1] * col[0] + a[3] * col[1] + col[3] + a[5] * col[4];
+                AtPA[4][c] = 0;
+                AtPA[5][c] = a[6] * col[4] + col[5];
+                AtPA[6][c] = 0;
+                AtPA[7][c] = 0;
+            }
+            T Pn[36];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+#pragma unroll
+                for (int j = 0; j <= i; ++j) {
+                    const T qv = (i < 6 && j < 6) ? Q[pidx(i, j)] : (T)0;
+                    Pn[pidx(i, j)] = qv + AtPA[i][j] + St[0][i] * K[0][j] + St[1][i] * K[1][j];
+                }
+            }
+            T At_h[6];
+            AT_mul(a, h, At_h);
+            T pn[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const T base = (i < 6) ? q[i] + At_h[i] : (T)0;
+                pn[i] = base + St[0][i] * kf0 + St[1][i] * kf1;
+            }
+            // store the record of stage k
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ws[L.ST(k, IpmLayout::RK + j)] = K[0][j];
+                ws[L.ST(k, IpmLayout::RK + 8 + j)] = K[1][j];
+            }
+            ws[L.ST(k, IpmLayout::RKFF)] = kf0;
+            ws[L.ST(k, IpmLayout::RKFF + 1)] = kf1;
+#pragma unroll
+            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pn[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pn[i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) ws[L.ST(k, IpmLayout::RA + i)] = a[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ws[L.ST(k, IpmLayout::RD + i)] = d[i];
+#pragma unroll
+            for (int i = 0; i < 36; ++i) Pm[i] = Pn[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pv[i] = pn[i];
+            unext[0] = u[0]; unext[1] = u[1];
+            if (k >= 1) { up[0] = um[0]; up[1] = um[1]; }
+        }
+        return true;
+    }
+
+    // -------------------------------------------------------- forward pass
+    // Step (dw) and new multipliers (YP) from the Riccati records; also the
+    // fraction-to-the-boundary step sizes, grad(phi)^T dw and the tiny-step measure.
+    struct Fwd {
+        T amax_p, amax_z, gd, rel;
+    };
+
+    MPCG_HD void dir_var(int i, T w, T lo, T hi, T gphi, T dwv, Fwd& F) const {
+        const T zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+        const T dl = w - lo, du = hi - w;
+        if (dwv < 0) F.amax_p = tmin(F.amax_p, -tau * dl / dwv);
+        if (dwv > 0) F.amax_p = tmin(F.amax_p, tau * du / dwv);
+        const T dzl = mu / dl - zl - zl / dl * dwv;
+        const T dzu = mu / du - zu + zu / du * dwv;
+        if (dzl < 0) F.amax_z = tmin(F.amax_z, -tau * zl / dzl);
+        if (dzu < 0) F.amax_z = tmin(F.amax_z, -tau * zu / dzu);
+        F.gd += gphi * dwv;
+        F.rel = tmax(F.rel, (T)fabs(dwv) / ((T)1 + (T)fabs(w)));
+    }
+
+    MPCG_HD Fwd forward(int mode) {
+        Fwd F{(T)1, (T)1, (T)0, (T)0};
+        T ds[8];
+        {
+            T s0[6];
+            load_s(0, s0);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) ds[j] = (mode == 0) ? -(s0[j] - pr.init[j]) : (T)0;
+            ds[6] = 0; ds[7] = 0;
+        }
+        T um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
+        if (N >= 2) load_u(0, u);
+        for (int k = 0; k < N; ++k) {
+            T Pm[36], pv[8];
+#pragma unroll
+            for (int i = 0; i < 36; ++i) Pm[i] = ws[L.ST(k, IpmLayout::RP + i)];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pv[i] = ws[L.ST(k, IpmLayout::Rp + i)];
+            // multipliers of rows (., k): yh+ = -(P ds + p)[0:6]
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                T acc = pv[j];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) acc += Pm[pidx(j, m)] * ds[m];
+                ws[L.YP(L.row(j, k))] = -acc;
+            }
+            T s[6];
+            load_s(k, s);
+            T g[6];
+            grad_state(s, g);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int i = L.vs(j, k);
+                ws[L.DW(i)] = ds[j];
+                if (mode == 0) {
+                    const T gphi = sf * g[j] - mu / (s[j] - sl) + mu / (su - s[j]);
+                    dir_var(i, s[j], sl, su, gphi, ds[j], F);
+                }
+            }
+            if (k == N - 1) break;
+            if (k + 1 < N - 1) load_u(k + 1, up);
+            T K[16], kf[2], a[7], d[6];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) K[i] = ws[L.ST(k, IpmLayout::RK + i)];
+            kf[0] = ws[L.ST(k, IpmLayout::RKFF)];
+            kf[1] = ws[L.ST(k, IpmLayout::RKFF + 1)];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) a[i] = ws[L.ST(k, IpmLayout::RA + i)];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) d[i] = ws[L.ST(k, IpmLayout::RD + i)];
+            T du0 = kf[0], du1 = kf[1];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                du0 += K[m] * ds[m];
+                du1 += K[8 + m] * ds[m];
+            }
+            const T duv[2] = {du0, du1};
+            T gu[2];
+            grad_ctrl(k, um, u, up, gu);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int i = L.vu(j, k);
+                ws[L.DW(i)] = duv[j];
+                if (mode == 0) {
+                    const T gphi = sf * gu[j] - mu / (u[j] - clo(j)) + mu / (chi(j) - u[j]);
+                    dir_var(i, u[j], clo(j), chi(j), gphi, duv[j], F);
+                }
+            }
+            T nx6[6];
+            A_mul(a, ds, nx6);
+            nx6[2] += dt * du0;
+            nx6[3] += dt * du1;
+            nx6[5] += dt * du0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) ds[j] = nx6[j] + d[j];
+            ds[6] = du0;
+            ds[7] = du1;
+            um[0] = u[0]; um[1] = u[1];
+            u[0] = up[0]; u[1] = up[1];
+        }
+        return F;
+    }
+
+    // ------------------------------------------------------------ trial point
+    // phi_mu and theta at w + alpha dw; returns false if outside the relaxed box.
+    MPCG_HD bool trial(T alpha, T* phi, T* th) const {
+        LogAcc<T> la;
+        la.init();
+        T f = 0, thv = 0;
+        T Fprev[6], um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
+        bool ok = true;
+        auto tv = [&](int i) -> T { return ws[L.W(i)] + alpha * ws[L.DW(i)]; };
+        if (N >= 2) { u[0] = tv(L.vu(0, 0)); u[1] = tv(L.vu(1, 0)); }
+        for (int k = 0; k < N; ++k) {
+            T s[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                s[j] = tv(L.vs(j, k));
+                const T dl = s[j] - sl, du = su - s[j];
+                ok = ok && (dl > 0) && (du > 0);
+                la.mul(dl);
+                la.mul(du);
+                const T c = k == 0 ? s[j] - pr.init[j] : s[j] - Fprev[j];
+                thv += fabs(rowscale(j, k) * c);
+            }
+            f += cost_state(s);
+            if (k == N - 1) break;
+            if (k + 1 < N - 1) { up[0] = tv(L.vu(0, k + 1)); up[1] = tv(L.vu(1, k + 1)); }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const T dl = u[j] - clo(j), du = chi(j) - u[j];
+                ok = ok && (dl > 0) && (du > 0);
+                la.mul(dl);
+                la.mul(du);
+            }
+            f += (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
+            if (k <= N - 3)
+                f += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
+            Lin<T> ln;
+            ln.eval(pr.c, s);
+            ln.next(s, u, dt, Fprev);
+            um[0] = u[0]; um[1] = u[1];
+            u[0] = up[0]; u[1] = up[1];
+        }
+        *phi = sf * f - mu * la.value();
+        *th = thv;
+        return ok && isfinite((double)*phi);
+    }
+
+    MPCG_HD void accept(T alpha, T amax_z) {
+        const T ksig = (T)1e10;
+        const int nx = L.nx();
+        for (int i = 0; i < nx; ++i) {
+            T lo, hi;
+            if (i < 6 * N) { lo = sl; hi = su; }
+            else if (i < 7 * N - 1) { lo = wl; hi = wu; }
+            else { lo = al; hi = au; }
+            const T w = ws[L.W(i)], dwv = ws[L.DW(i)], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+            const T dl = w - lo, du = hi - w;
+            const T dzl = mu / dl - zl - zl / dl * dwv;
+            const T dzu = mu / du - zu + zu / du * dwv;
+            const T wn = w + alpha * dwv;
+            const T sl2 = wn - lo, su2 = hi - wn;
+            T zln = zl + amax_z * dzl, zun = zu + amax_z * dzu;
+            zln = tmax(tmin(zln, ksig * mu / sl2), mu / (ksig * sl2));
+            zun = tmax(tmin(zun, ksig * mu / su2), mu / (ksig * su2));
+            ws[L.W(i)] = wn;
+            ws[L.ZL(i)] = zln;
+            ws[L.ZU(i)] = zun;
+        }
+        const int ng = L.ng();
+        for (int r = 0; r < ng; ++r) {
+            const T y = ws[L.Y(r)];
+            ws[L.Y(r)] = y + alpha * (ws[L.YP(r)] - y);
+        }
+    }
+
+    // ------------------------------------------------------------------ solve
+    MPCG_HD IpmResult solve() {
+        setup();
+        init_point();
+        // least-squares multipliers (constr_mult_init_max 1000)
+        {
+            bool ok = riccati(1, (T)0);
+            T ymax = 0;
+            if (ok) {
+                forward(1);
+                for (int k = 0; k < N; ++k)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) ymax = tmax(ymax, (T)fabs(ws[L.YP(L.row(j, k))] / rowscale(j, k)));
+            }
+            const bool use = ok && ymax <= (T)1000;
+            for (int r = 0; r < L.ng(); ++r) ws[L.Y(r)] = use ? ws[L.YP(r)] : (T)0;
+        }
+        mu = (T)P.mu_init;
+        const T mu_min = (T)(P.tol / 10.0);
+        tau = tmax((T)0.99, (T)1 - mu);
+        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
+        const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
+        stats();
+        const T theta0 = theta;
+        const T theta_max = (T)1e4 * tmax((T)1, theta0);
+        const T theta_min = (T)1e-4 * tmax((T)1, theta0);
+        T delta_w_last = 0;
+        nfilter = 0;
+        const int cap = P.filter_cap;
+        IpmResult res{IPM_MAXITER, 0, 0.0, 0.0};
+        int iter = 0;
+        const int nbnd = 2 * L.nx();
+        const int ng = L.ng();
+        for (iter = 0; iter <= P.max_iter; ++iter) {
+            if (iter > 0) stats();
+            const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
+            const T sc = tmax((T)100, l1z / (T)nbnd) / (T)100;
+            const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / sc));
+            const T dual_uns = dual_inf / sf;
+            res.kkt_inf = (double)tmax(dual_uns, tmax(prim_uns, compl0));
+            if (!isfinite((double)E0)) { res.status = IPM_INVALID_NUMBER; break; }
+            if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4) {
+                res.status = IPM_SUCCESS;
+                break;
+            }
+            if (iter == P.max_iter) { res.status = IPM_MAXITER; break; }
+            // monotone barrier update (possibly several times)
+            for (;;) {
+                const T complmu = tmax(pmax - mu, mu - pmin);
+                const T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / sc));
+                if (Emu > kappa_eps * mu || mu <= mu_min) break;
+                const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
+                if (mnew >= mu) break;
+                mu = mnew;
+                tau = tmax((T)0.99, (T)1 - mu);
+                nfilter = 0;
+            }
+            // Newton step with inertia correction
+            T delta_w = 0;
+            int attempt = 0;
+            bool ok = false;
+            for (;;) {
+                if (riccati(0, delta_w)) {
+                    ok = true;
+                    if (delta_w > 0) delta_w_last = delta_w;
+                    break;
+                }
+                if (attempt == 0)
+                    delta_w = (delta_w_last == 0) ? (T)1e-4 : tmax((T)1e-20, delta_w_last / (T)3);
+                else
+                    delta_w = (delta_w_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
+                ++attempt;
+                if (delta_w > (T)1e40) break;
+            }
+            if (!ok) { res.status = IPM_ERROR_IN_STEP; break; }
+            const Fwd Fd = forward(0);
+            // filter line search
+            const T phik = sf * fval - mu * logsum;
+            const T thetak = theta;
+            const T gd = Fd.gd;
+            T alpha_min;
+            if (gd < 0 && thetak <= theta_min)
+                alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd,
+                                                                 delta_sw * (T)pow((double)thetak, (double)s_theta) /
+                                                                     (T)pow((double)-gd, (double)s_phi)));
+            else if (gd < 0)
+                alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
+            else
+                alpha_min = gamma_alpha * gamma_theta;
+            const bool tiny = Fd.rel < (T)(10.0 * 2.2e-16);
+            T alpha = Fd.amax_p;
+            bool accepted = false, ftype = false;
+            for (int ls = 0; ls < 60; ++ls) {
+                if (tiny) { accepted = true; ftype = true; break; }
+                if (alpha < alpha_min) break;
+                T phit, thetat;
+                const bool okt = trial(alpha, &phit, &thetat);
+                if (okt && thetat < theta_max) {
+                    bool infilt = false;
+                    for (int f = 0; f < nfilter; ++f) {
+                        const T fth = ws[L.FI(2 * f)], fph = ws[L.FI(2 * f + 1)];
+                        if (thetat >= fth && phit >= fph) { infilt = true; break; }
+                    }
+                    if (!infilt) {
+                        const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
+                                                     delta_sw * (T)pow((double)thetak, (double)s_theta));
+                        if (thetak <= theta_min && sw) {
+                            if (phit <= phik + eta_phi * alpha * gd) { accepted = true; ftype = true; break; }
+                        } else if (thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak) {
+                            accepted = true;
+                            ftype = false;
+                            break;
+                        }
+                    }
+                }
+                alpha *= (T)0.5;
+            }
+            if (!accepted) { res.status = IPM_RESTORATION_FAILURE; break; }
+            if (!ftype) {
+                int slot = nfilter;
+                if (nfilter == cap) {  // full: drop the oldest entry
+                    for (int f = 1; f < cap; ++f) {
+                        ws[L.FI(2 * (f - 1))] = ws[L.FI(2 * f)];
+                        ws[L.FI(2 * (f - 1) + 1)] = ws[L.FI(2 * f + 1)];
+                    }
+                    slot = cap - 1;
+                } else {
+                    ++nfilter;
+                }
+                ws[L.FI(2 * slot)] = ((T)1 - gamma_theta) * thetak;
+                ws[L.FI(2 * slot + 1)] = phik - gamma_phi * thetak;
+            }
+            accept(alpha, Fd.amax_z);
+        }
+        res.iters = iter;
+        return res;
+    }
+
+    // Final point with honor_original_bounds projection; objective at that point.
+    MPCG_HD T x_out(int i) const {
+        T v = ws[L.W(i)];
+        T lo, hi;
+        if (i < 6 * N) { lo = sl0; hi = su0; }
+        else if (i < 7 * N - 1) { lo = wl0; hi = wu0; }
+        else { lo = al0; hi = au0; }
+        return tmin(tmax(v, lo), hi);
+    }
+    MPCG_HD T objective_out() const {
+        T f = 0;
+        for (int k = 0; k < N; ++k) {
+            T s[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) s[j] = x_out(L.vs(j, k));
+            f += cost_state(s);
+        }
+        for (int k = 0; k < N - 1; ++k) {
+            const T w = x_out(L.vu(0, k)), a = x_out(L.vu(1, k));
+            f += (T)P.w_w * w * w + (T)P.w_a * a * a;
+            if (k <= N - 3) {
+                const T w1 = x_out(L.vu(0, k + 1)), a1 = x_out(L.vu(1, k + 1));
+                f += (T)P.w_dw * (w1 - w) * (w1 - w) + (T)P.w_da * (a1 - a) * (a1 - a);
+            }
+        }
+        return f;
+    }
+};
+
+}  // namespace mpcg
+#endif
