@@ -1,0 +1,191 @@
+"""Benchmark: NMPC solves/s of the MPC::Solve hot path on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --horizon N]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (multi-GPU)
+
+A step = one pass of the hot path over one batch: every rank solves its shard of
+B problems (BASELINE.json configs[3]: 524288 problems over 8 GPUs = 65536 per GPU,
+N = 20, fp64, differential drive) with the HIP kernel, then the controls and
+statuses are gathered to rank 0 (RCCL all-gather over xGMI) -- the only
+collective.  Inputs are resident in HBM before the timed region (weak scaling: the
+per-GPU batch is fixed).  Rank 0 prints one JSON line.
+
+roofline: the dominant (only) kernel, ipm_solve_kernel.  achieved = algorithmic
+bytes per launch (B x 8 x (6 + 4 + 2 + 3N) = B x 576 B at N = 20)
+divided by the kernel's average duration measured with HIP events on the stream
+it runs on; traffic = HBM bytes per launch from the committed rocprofv3 PMC
+summary for this configuration (profiles/), or null.
+cpu_baseline: the oracle (dense Ipopt restatement, "port") on a bounded sample of
+the same problems, rank 0, N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=65536, help="problems per GPU")
+    ap.add_argument("--horizon", type=int, default=20)
+    ap.add_argument("--gather-traj", action="store_true", help="also gather the 3N trajectories")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (0 = skip)")
+    ap.add_argument("--profile-name", default=None, help="PMC summary to read traffic from")
+    return ap.parse_args()
+
+
+def cpu_baseline(P, st, cf, budget_s):
+    """Oracle (Ipopt restatement, dense KKT) timed on the host cores."""
+    from oracle import pyoracle as O
+
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    opts = O.ipm_opts(tol=1e-8)
+    n = threads * 2
+    t0 = time.perf_counter()
+    O.mpc_solve_batch(P, st[:n], cf[:n], opts=opts, nthreads=threads)
+    dt = time.perf_counter() - t0
+    per = dt / n
+    m = int(max(n, min(len(st), budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    r = O.mpc_solve_batch(P, st[:m], cf[:m], opts=opts, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=m / dt, unit="solves/s", cores=threads, kind="port",
+                sample=f"first {m} problems of the benchmark batch, oracle/ipm.c (Ipopt 3.12 algorithm, dense "
+                       f"Bunch-Kaufman KKT), {threads} OpenMP threads, {dt:.1f} s",
+                iters_mean=float(np.mean(r["iters"])))
+
+
+def pmc_traffic(name):
+    path = os.path.join(ROOT, "profiles", f"{name}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from mpc_ros_amd import dist as D
+    from mpc_ros_amd import infinity, params
+    from mpc_ros_amd.solver import BatchSolver
+
+    rank, world, local = D.env_rank_world()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    N = a.horizon
+    B = a.batch
+    total = B * world
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=N)
+    start, count = D.shard(total, rank, world)
+    st, cf = infinity.make_problems(np.arange(start, start + count))
+    tst = torch.from_numpy(st).to(dev)
+    tcf = torch.from_numpy(cf).to(dev)
+    solver = BatchSolver(dev.index, P)
+    solver.reserve(count)
+    u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
+    traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)
+    status = torch.empty(count, dtype=torch.int32, device=dev)
+    iters = torch.empty(count, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    k_ms = []
+
+    def step(timed):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        solver.solve_device(tst, tcf, u0, traj, status, None, iters, stream=stream)
+        if timed:
+            e1.record(stream)
+            k_ms.append((e0, e1))
+        if world > 1:
+            g_u0 = D.gather_rows(u0, total)
+            g_st = D.gather_rows(status, total)
+            if a.gather_traj:
+                D.gather_rows(traj.view(count, -1), total)
+            return g_u0, g_st
+        return u0, status
+
+    for _ in range(a.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern = float(np.mean([e0.elapsed_time(e1) for e0, e1 in k_ms])) if k_ms else float("nan")
+    if world > 1:
+        t = torch.tensor([elapsed, kern], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern = float(t[0]), float(t[1])
+    it = iters.cpu().numpy()
+    sts = status.cpu().numpy()
+    if rank == 0:
+        value = total * a.steps / elapsed
+        bytes_per_solve = 8 * (6 + 4 + 2 + 3 * N)
+        achieved = count * bytes_per_solve / (kern * 1e-3) / 1e9
+        prof = a.profile_name or f"pmc_B{B}_N{N}"
+        traffic = pmc_traffic(prof)
+        line = {
+            "metric": "NMPC solves/sec (whole node), N=20 diff-drive, at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem)",
+            "config": {"workload": f"diff-drive NMPC (MPC::Solve NLP, Ipopt algorithm), N={N}, fp64, "
+                                   f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
+                       "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ipm_solve_kernel", "kernel_ms": kern,
+                         "algorithmic_bytes_per_solve": bytes_per_solve},
+            "solver": {"iters_mean": float(it.mean()), "iters_max": int(it.max()),
+                       "success_frac": float(np.mean(sts == 1))},
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(P, st, cf, a.cpu_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

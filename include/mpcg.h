@@ -1,0 +1,122 @@
+/*
+ * include/mpcg.h -- C-ABI of the MI355X batched NMPC solver (libmpcg.so).
+ *
+ * Drop-in boundary for the hot path of OkDoky/mpc_ros: the call
+ *     vector<double> MPC::Solve(Eigen::VectorXd state, Eigen::VectorXd coeffs)
+ * (mpc_ros/include/mpc_planner.h:31, mpc_ros/src/mpc_planner.cpp:265-402), which
+ * tapes FG_eval with CppAD and solves the NLP with Ipopt 3.12.8 through
+ * CppAD::ipopt::solve (mpc_ros/include/cppad/ipopt/solve.hpp:419-589).  Here a
+ * batch of B independent problems is solved on one GPU by hand-written CDNA4 HIP
+ * kernels running the same interior-point algorithm (mpc_ros_amd/csrc/ipm_core.h).
+ *
+ * Plain C types only; every pointer is caller-owned.  Return codes: 0 = ok,
+ * negative = API / HIP error (message in mpcg_last_error()).  Per-problem solver
+ * outcomes are reported in `status` with CppAD::ipopt::solve_result::status_type
+ * numbering (mpc_ros/include/cppad/ipopt/solve_result.hpp:30-46): 1 success,
+ * 2 maxiter_exceeded, 9 restoration_failure, 10 error_in_step_computation,
+ * 11 invalid_number_detected.  As in the reference (mpc_planner.cpp:378, the
+ * status is computed and then ignored), the last iterate is always returned.
+ *
+ * Threading: one handle per thread; mpcg_set_params must not run concurrently with
+ * a solve on the same handle (the reference has an unsynchronised writer here,
+ * SURVEY.md §3.3 -- this API makes the ordering the caller's explicit job).
+ *
+ * Integration (cgo/ctypes/C++ stubs): INTEGRATION.md.
+ */
+#ifndef MPCG_H
+#define MPCG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCG_ABI_VERSION 1
+
+/* The 15 keys of the reference's parameter map (DrivingStateContext::updateMpcConfigs,
+ * mpc_ros/src/driving_state.cpp:65-79; MPC::LoadParams mpc_planner.cpp:243-262;
+ * FG_eval::LoadParams mpc_planner.cpp:71-97), plus the Ipopt options the reference
+ * leaves at their defaults (mpc_planner.cpp:356-368). */
+typedef struct mpcg_params {
+    int32_t steps;            /* "STEPS": horizon N (double truncated to int, :74, :247) */
+    int32_t model;            /* 0 = differential drive (FG_eval); 1 = kinematic bicycle */
+    double dt;                /* "DT" */
+    double ref_cte;           /* "REF_CTE" */
+    double ref_etheta;        /* "REF_ETHETA" */
+    double ref_v;             /* "REF_V" */
+    double w_cte;             /* "W_CTE" */
+    double w_etheta;          /* "W_EPSI" */
+    double w_v;               /* "W_V" */
+    double w_angvel;          /* "W_ANGVEL" */
+    double w_accel;           /* "W_A" */
+    double w_angvel_d;        /* "W_DANGVEL" */
+    double w_accel_d;         /* "W_DA" */
+    double max_angvel;        /* "ANGVEL" */
+    double max_throttle;      /* "MAXTHR" */
+    double bound;             /* "BOUND" */
+    /* Ipopt 3.12 defaults unless changed */
+    double tol;               /* 1e-8 */
+    int32_t max_iter;         /* 3000 */
+    int32_t filter_cap;       /* filter entries kept per problem (64) */
+    double bound_relax_factor;/* 1e-8 */
+    double mu_init;           /* 0.1 */
+    double wheelbase;         /* model 1 only: Lf [m] */
+} mpcg_params;
+
+typedef struct mpcg_handle mpcg_handle;
+
+int mpcg_abi_version(void);
+const char* mpcg_last_error(void);
+
+/* Defaults of an MPC object before LoadParams: MPC::MPC() (mpc_planner.cpp:223-241)
+ * + FG_eval constructor (:42-68). */
+int mpcg_params_default(mpcg_params* p);
+/* Defaults the move_base plugin loads (mpc_ros/cfg/MPCPlanner.cfg:22-37, DT 0.1). */
+int mpcg_params_plugin_default(mpcg_params* p);
+/* One LoadParams map entry: key is one of the 15 reference keys.
+ * Returns 0 if applied, 1 if the key is unknown (ignored, as LoadParams ignores it). */
+int mpcg_params_set(mpcg_params* p, const char* key, double value);
+/* Validate a parameter set (steps >= 2, dt > 0, bounds > 0, weights >= 0). */
+int mpcg_params_check(const mpcg_params* p);
+
+/* Handle bound to one GPU (HIP device ordinal). */
+int mpcg_create(int device, mpcg_handle** out);
+void mpcg_destroy(mpcg_handle* h);
+int mpcg_set_params(mpcg_handle* h, const mpcg_params* p);
+int mpcg_get_params(const mpcg_handle* h, mpcg_params* p);
+/* Device workspace for B problems (bytes); reserve it ahead of graph capture. */
+size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B);
+int mpcg_reserve(mpcg_handle* h, int64_t B);
+
+/* Batched solve, host buffers, synchronous (copies in, solves, copies out).
+ *   state  [B][6]  x, y, theta, v, cte, etheta   (MPC::Solve `state`)
+ *   coeffs [B][4]  c0..c3                        (MPC::Solve `coeffs`)
+ *   u0     [B][2]  omega_0, a_0                  (MPC::Solve return value)
+ *   traj   [B][3][N] mpc_x | mpc_y | mpc_theta   (MPC::mpc_x/mpc_y/mpc_theta) or NULL
+ *   status [B] or NULL, obj [B] or NULL, iters [B] or NULL */
+int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0,
+               double* traj, int32_t* status, double* obj, int32_t* iters);
+
+/* Batched solve on device-resident buffers (same layouts), asynchronous on `stream`
+ * (a hipStream_t; NULL = the handle's own stream).  No host synchronisation, no
+ * allocation if mpcg_reserve(h, B) was called: safe to capture in a HIP graph. */
+int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
+                      double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
+
+/* Fused pre-processing + solve: Tracking::findBestPath (driving_state.cpp:175-256)
+ * on device for B robots, then the solve.  pose [B][3] (x, y, yaw), vel [B][3]
+ * (v feedback, previous w, previous throttle), plan [B][M][2] waypoints.
+ * Writes state/coeffs (optional, may be NULL) and the solve outputs. */
+int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
+                           const double* d_plan, int32_t delay_mode, double* d_state, double* d_coeffs,
+                           void* stream);
+
+/* Wait for all work queued on the handle's stream. */
+int mpcg_synchronize(mpcg_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,324 @@
+// mpc_ros_amd/csrc/mpcg_api.cpp -- the C-ABI of include/mpcg.h.
+//
+// Owns device buffers and a stream per handle; translates the reference's
+// parameter map semantics (MPC::LoadParams / FG_eval::LoadParams,
+// mpc_ros/src/mpc_planner.cpp:71-97, 243-262) into the kernel's IpmParams.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "mpcg.h"
+#include "mpcg_internal.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(-2, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+struct mpcg_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    mpcg_params params{};
+    double* ws = nullptr;
+    size_t ws_bytes = 0;
+    // staging buffers for mpcg_solve (host pointers)
+    double* d_io = nullptr;
+    size_t io_bytes = 0;
+};
+
+extern "C" {
+
+int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
+const char* mpcg_last_error(void) { return g_err.c_str(); }
+
+static void ipopt_defaults(mpcg_params* p) {
+    p->tol = 1e-8;
+    p->max_iter = 3000;
+    p->filter_cap = 64;
+    p->bound_relax_factor = 1e-8;
+    p->mu_init = 0.1;
+    p->wheelbase = 0.5;
+    p->model = 0;
+}
+
+int mpcg_params_default(mpcg_params* p) {
+    if (!p) return fail(-1, "null params");
+    std::memset(p, 0, sizeof *p);
+    // MPC::MPC() (mpc_planner.cpp:223-241)
+    p->steps = 20;
+    p->max_angvel = 3.0;
+    p->max_throttle = 1.0;
+    p->bound = 1.0e3;
+    // FG_eval::FG_eval (mpc_planner.cpp:42-68)
+    p->dt = 0.1;
+    p->ref_cte = 0.0;
+    p->ref_etheta = 0.0;
+    p->ref_v = 0.5;
+    p->w_cte = 100;
+    p->w_etheta = 100;
+    p->w_v = 1;
+    p->w_angvel = 100;
+    p->w_accel = 50;
+    p->w_angvel_d = 0;
+    p->w_accel_d = 0;
+    ipopt_defaults(p);
+    return 0;
+}
+
+int mpcg_params_plugin_default(mpcg_params* p) {
+    if (!p) return fail(-1, "null params");
+    std::memset(p, 0, sizeof *p);
+    // mpc_ros/cfg/MPCPlanner.cfg:22-37; DT = 1/controller_frequency (driving_state.cpp:28)
+    p->steps = 20;
+    p->dt = 0.1;
+    p->ref_cte = 0.0;
+    p->ref_etheta = 0.0;
+    p->ref_v = 1.0;
+    p->w_cte = 1000;
+    p->w_etheta = 1000;
+    p->w_v = 100;
+    p->w_angvel = 100;
+    p->w_accel = 50;
+    p->w_angvel_d = 0;
+    p->w_accel_d = 10;
+    p->max_angvel = 1.0;
+    p->max_throttle = 1.0;
+    p->bound = 1000;
+    ipopt_defaults(p);
+    return 0;
+}
+
+int mpcg_params_set(mpcg_params* p, const char* key, double v) {
+    if (!p || !key) return fail(-1, "null argument");
+    const std::string k(key);
+    if (k == "DT") p->dt = v;
+    else if (k == "STEPS") p->steps = (int32_t)v;  // double -> int truncation, as the reference
+    else if (k == "REF_CTE") p->ref_cte = v;
+    else if (k == "REF_ETHETA") p->ref_etheta = v;
+    else if (k == "REF_V") p->ref_v = v;
+    else if (k == "W_CTE") p->w_cte = v;
+    else if (k == "W_EPSI") p->w_etheta = v;
+    else if (k == "W_V") p->w_v = v;
+    else if (k == "W_ANGVEL") p->w_angvel = v;
+    else if (k == "W_A") p->w_accel = v;
+    else if (k == "W_DANGVEL") p->w_angvel_d = v;
+    else if (k == "W_DA") p->w_accel_d = v;
+    else if (k == "ANGVEL") p->max_angvel = v;
+    else if (k == "MAXTHR") p->max_throttle = v;
+    else if (k == "BOUND") p->bound = v;
+    else return 1;
+    return 0;
+}
+
+int mpcg_params_check(const mpcg_params* p) {
+    if (!p) return fail(-1, "null params");
+    if (p->steps < 2 || p->steps > 4096) return fail(-1, "STEPS must be in [2, 4096]");
+    if (!(p->dt > 0) || !std::isfinite(p->dt)) return fail(-1, "DT must be > 0");
+    if (!(p->max_angvel > 0) || !(p->max_throttle > 0) || !(p->bound > 0)) return fail(-1, "bounds must be > 0");
+    const double w[] = {p->w_cte, p->w_etheta, p->w_v, p->w_angvel, p->w_accel, p->w_angvel_d, p->w_accel_d};
+    for (double x : w)
+        if (!(x >= 0) || !std::isfinite(x)) return fail(-1, "weights must be finite and >= 0");
+    if (!(p->tol > 0)) return fail(-1, "tol must be > 0");
+    if (p->max_iter < 0) return fail(-1, "max_iter must be >= 0");
+    if (p->filter_cap < 1 || p->filter_cap > 1024) return fail(-1, "filter_cap must be in [1, 1024]");
+    if (!(p->bound_relax_factor >= 0) || !(p->mu_init > 0)) return fail(-1, "invalid Ipopt options");
+    if (p->model != 0) return fail(-1, "model: only 0 (differential drive) is implemented");
+    return 0;
+}
+
+static mpcg::IpmParams to_ipm(const mpcg_params& p) {
+    mpcg::IpmParams q{};
+    q.N = p.steps;
+    q.dt = p.dt;
+    q.ref_cte = p.ref_cte;
+    q.ref_eth = p.ref_etheta;
+    q.ref_v = p.ref_v;
+    q.w_cte = p.w_cte;
+    q.w_eth = p.w_etheta;
+    q.w_v = p.w_v;
+    q.w_w = p.w_angvel;
+    q.w_a = p.w_accel;
+    q.w_dw = p.w_angvel_d;
+    q.w_da = p.w_accel_d;
+    q.max_w = p.max_angvel;
+    q.max_a = p.max_throttle;
+    q.bound = p.bound;
+    q.tol = p.tol;
+    q.bound_relax_factor = p.bound_relax_factor;
+    q.mu_init = p.mu_init;
+    q.max_iter = p.max_iter;
+    q.filter_cap = p.filter_cap;
+    return q;
+}
+
+size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B) {
+    if (!p || B <= 0) return 0;
+    const mpcg::IpmLayout L{p->steps};
+    return (size_t)L.total(p->filter_cap) * sizeof(double) * (size_t)B;
+}
+
+int mpcg_create(int device, mpcg_handle** out) {
+    if (!out) return fail(-1, "null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    if (device < 0 || device >= n) return fail(-3, "device ordinal out of range (no GPU?)");
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    mpcg_handle* h = new mpcg_handle();
+    h->device = device;
+    e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    mpcg_params_plugin_default(&h->params);
+    *out = h;
+    return 0;
+}
+
+void mpcg_destroy(mpcg_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->ws) hipFree(h->ws);
+    if (h->d_io) hipFree(h->d_io);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int mpcg_set_params(mpcg_handle* h, const mpcg_params* p) {
+    if (!h || !p) return fail(-1, "null argument");
+    int rc = mpcg_params_check(p);
+    if (rc) return rc;
+    h->params = *p;
+    return 0;
+}
+
+int mpcg_get_params(const mpcg_handle* h, mpcg_params* p) {
+    if (!h || !p) return fail(-1, "null argument");
+    *p = h->params;
+    return 0;
+}
+
+static int ensure_ws(mpcg_handle* h, int64_t B) {
+    const size_t need = mpcg_workspace_bytes(&h->params, B);
+    if (need <= h->ws_bytes) return 0;
+    hipSetDevice(h->device);
+    if (h->ws) {
+        hipStreamSynchronize(h->stream);
+        hipFree(h->ws);
+        h->ws = nullptr;
+        h->ws_bytes = 0;
+    }
+    hipError_t e = hipMalloc((void**)&h->ws, need);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+    h->ws_bytes = need;
+    return 0;
+}
+
+int mpcg_reserve(mpcg_handle* h, int64_t B) {
+    if (!h) return fail(-1, "null handle");
+    if (B < 0) return fail(-1, "negative batch");
+    return ensure_ws(h, B);
+}
+
+int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
+                      double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream) {
+    if (!h) return fail(-1, "null handle");
+    if (B < 0) return fail(-1, "negative batch");
+    if (B == 0) return 0;
+    if (!d_state || !d_coeffs || !d_u0) return fail(-1, "state, coeffs and u0 are required");
+    int rc = mpcg_params_check(&h->params);
+    if (rc) return rc;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    rc = ensure_ws(h, B);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    e = mpcg::launch_ipm_solve(to_ipm(h->params), B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,
+                               h->ws, s);
+    if (e != hipSuccess) return hip_fail(e, "ipm_solve_kernel launch");
+    return 0;
+}
+
+int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
+               int32_t* status, double* obj, int32_t* iters) {
+    if (!h) return fail(-1, "null handle");
+    if (B < 0) return fail(-1, "negative batch");
+    if (B == 0) return 0;
+    if (!state || !coeffs || !u0) return fail(-1, "state, coeffs and u0 are required");
+    int rc = mpcg_params_check(&h->params);
+    if (rc) return rc;
+    const int N = h->params.steps;
+    // io block: state 6 | coeffs 4 | u0 2 | traj 3N | obj 1 | status+iters (2 int32 = 1 double)
+    const size_t per = (size_t)(6 + 4 + 2 + 3 * N + 1 + 1);
+    const size_t need = per * sizeof(double) * (size_t)B;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (need > h->io_bytes) {
+        if (h->d_io) {
+            hipStreamSynchronize(h->stream);
+            hipFree(h->d_io);
+            h->d_io = nullptr;
+            h->io_bytes = 0;
+        }
+        e = hipMalloc((void**)&h->d_io, need);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(io)");
+        h->io_bytes = need;
+    }
+    double* ds = h->d_io;
+    double* dc = ds + 6 * B;
+    double* du = dc + 4 * B;
+    double* dt = du + 2 * B;
+    double* dob = dt + (size_t)3 * N * B;
+    int32_t* dst = (int32_t*)(dob + B);
+    int32_t* dit = dst + B;
+    e = hipMemcpyAsync(ds, state, sizeof(double) * 6 * B, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dc, coeffs, sizeof(double) * 4 * B, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy H2D");
+    rc = mpcg_solve_device(h, B, ds, dc, du, dt, dst, dob, dit, h->stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(u0, du, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && traj)
+        e = hipMemcpyAsync(traj, dt, sizeof(double) * 3 * N * B, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && obj) e = hipMemcpyAsync(obj, dob, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && status)
+        e = hipMemcpyAsync(status, dst, sizeof(int32_t) * B, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && iters)
+        e = hipMemcpyAsync(iters, dit, sizeof(int32_t) * B, hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy D2H");
+    e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
+                           const double* d_plan, int32_t delay_mode, double* d_state, double* d_coeffs,
+                           void* stream) {
+    (void)B; (void)M; (void)d_pose; (void)d_vel; (void)d_plan; (void)delay_mode; (void)d_state; (void)d_coeffs;
+    (void)stream;
+    if (!h) return fail(-1, "null handle");
+    return fail(-4, "mpcg_preprocess_device: not built in this version");
+}
+
+int mpcg_synchronize(mpcg_handle* h) {
+    if (!h) return fail(-1, "null handle");
+    hipSetDevice(h->device);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+}  // extern "C"

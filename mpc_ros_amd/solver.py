@@ -1,0 +1,94 @@
+"""Batched NMPC solver on one MI355X (wrapper of the C-ABI in include/mpcg.h).
+
+``BatchSolver`` owns one ``mpcg_handle`` (one GPU).  ``solve`` takes host numpy
+arrays; ``solve_device`` takes torch tensors already resident in HBM and queues
+the kernel on the current torch stream without any host synchronisation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .params import PLUGIN_DEFAULTS
+
+# Ipopt options the reference leaves at their defaults (mpc_planner.cpp:356-368)
+IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor=1e-8, mu_init=0.1)
+
+
+class BatchSolver:
+    def __init__(self, device: int = 0, params: dict | None = None, **ipopt):
+        L = _lib.lib()
+        h = C.c_void_p()
+        _lib.check(L.mpcg_create(int(device), C.byref(h)), "mpcg_create")
+        self._h = h
+        self.device = device
+        self.set_params(params if params is not None else PLUGIN_DEFAULTS, **ipopt)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().mpcg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ parameters
+    def set_params(self, params: dict, base: str = "plugin", **ipopt):
+        p = _lib.params_from_map(params, base)
+        opts = dict(IPOPT_DEFAULTS)
+        opts.update(ipopt)
+        for k, v in opts.items():
+            setattr(p, k, v)
+        _lib.check(_lib.lib().mpcg_set_params(self._h, C.byref(p)), "mpcg_set_params")
+        self.params = p
+        self.N = p.steps
+
+    def reserve(self, B: int):
+        _lib.check(_lib.lib().mpcg_reserve(self._h, int(B)), "mpcg_reserve")
+
+    def workspace_bytes(self, B: int) -> int:
+        return int(_lib.lib().mpcg_workspace_bytes(C.byref(self.params), int(B)))
+
+    # ----------------------------------------------------------------- solve
+    def solve(self, state: np.ndarray, coeffs: np.ndarray, want_traj: bool = True) -> dict:
+        state = np.ascontiguousarray(state, dtype=np.float64)
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+        B = state.shape[0]
+        assert state.shape == (B, 6) and coeffs.shape == (B, 4), "state [B,6], coeffs [B,4]"
+        N = self.N
+        u0 = np.zeros((B, 2))
+        traj = np.zeros((B, 3, N)) if want_traj else None
+        status = np.zeros(B, dtype=np.int32)
+        iters = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int32)
+        _lib.check(_lib.lib().mpcg_solve(
+            self._h, B, state.ctypes.data_as(dp), coeffs.ctypes.data_as(dp), u0.ctypes.data_as(dp),
+            traj.ctypes.data_as(dp) if traj is not None else None, status.ctypes.data_as(ip),
+            obj.ctypes.data_as(dp), iters.ctypes.data_as(ip)), "mpcg_solve")
+        return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters)
+
+    def solve_device(self, state, coeffs, u0, traj=None, status=None, obj=None, iters=None, stream=None):
+        """All arguments are torch tensors on this handle's GPU (float64 / int32, contiguous)."""
+        import torch
+
+        B = state.shape[0]
+        for t, shape, dt in ((state, (B, 6), torch.float64), (coeffs, (B, 4), torch.float64),
+                             (u0, (B, 2), torch.float64)):
+            assert t.is_cuda and t.dtype == dt and t.is_contiguous() and tuple(t.shape) == shape
+        if traj is not None:
+            assert traj.dtype == torch.float64 and traj.is_contiguous() and traj.numel() == B * 3 * self.N
+        for t in (status, iters):
+            assert t is None or (t.dtype == torch.int32 and t.numel() == B)
+        if stream is None:
+            stream = torch.cuda.current_stream(state.device)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        _lib.check(_lib.lib().mpcg_solve_device(
+            self._h, B, ptr(state), ptr(coeffs), ptr(u0), ptr(traj), ptr(status), ptr(obj), ptr(iters),
+            C.c_void_p(stream.cuda_stream)), "mpcg_solve_device")

@@ -1,0 +1,119 @@
+"""The C-ABI library: loads, exports every symbol include/*.h declares, parameter
+handling -- all without a GPU (no compute calls here)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_functions(header: str) -> list[str]:
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpcg_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported(libmpcg):
+    from mpc_ros_amd import _lib
+
+    names = declared_functions("mpcg.h")
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(libmpcg, n), n
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes signature table"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    # class MPC (include/mpc_planner.h): ctor, LoadParams, SolveRaw behind the Solve template, SolveBatch
+    for mangled in ("_ZN3MPCC1Ev", "_ZN3MPC10LoadParams", "_ZN3MPC8SolveRawEPKdS1_", "_ZN3MPC10SolveBatch",
+                    "_ZN3MPCD1Ev"):
+        assert mangled in out, mangled
+
+
+def test_abi_version_and_struct_size(libmpcg):
+    from mpc_ros_amd import _lib
+
+    assert libmpcg.mpcg_abi_version() == 1
+    # C struct layout: compile a tiny probe against the header and compare sizeof/offsets
+    src = ("#include <stdio.h>\n#include <stddef.h>\n#include \"mpcg.h\"\nint main(){printf(\"%zu %zu %zu %zu\","
+           "sizeof(mpcg_params),offsetof(mpcg_params,tol),offsetof(mpcg_params,filter_cap),"
+           "offsetof(mpcg_params,wheelbase));}\n")
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "p.c"), "w").write(src)
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(d, "p"),
+                               os.path.join(d, "p.c")])
+        got = [int(v) for v in subprocess.check_output([os.path.join(d, "p")]).split()]
+    P = _lib.MpcgParams
+    assert got == [C.sizeof(P), P.tol.offset, P.filter_cap.offset, P.wheelbase.offset]
+
+
+def test_param_defaults_and_keys(libmpcg):
+    from mpc_ros_amd import _lib
+
+    p = _lib.MpcgParams()
+    assert libmpcg.mpcg_params_default(C.byref(p)) == 0
+    assert (p.steps, p.max_angvel, p.max_throttle, p.bound) == (20, 3.0, 1.0, 1000.0)
+    assert (p.dt, p.ref_v, p.w_cte, p.w_etheta, p.w_v, p.w_angvel, p.w_accel) == (0.1, 0.5, 100, 100, 1, 100, 50)
+    assert (p.tol, p.max_iter, p.bound_relax_factor, p.mu_init) == (1e-8, 3000, 1e-8, 0.1)
+    assert libmpcg.mpcg_params_plugin_default(C.byref(p)) == 0
+    assert (p.ref_v, p.w_cte, p.w_accel_d, p.max_angvel) == (1.0, 1000, 10, 1.0)
+    assert libmpcg.mpcg_params_set(C.byref(p), b"STEPS", 33.7) == 0 and p.steps == 33
+    assert libmpcg.mpcg_params_set(C.byref(p), b"W_EPSI", 12.0) == 0 and p.w_etheta == 12.0
+    assert libmpcg.mpcg_params_set(C.byref(p), b"NOT_A_KEY", 1.0) == 1
+    assert libmpcg.mpcg_params_check(C.byref(p)) == 0
+    p.steps = 1
+    assert libmpcg.mpcg_params_check(C.byref(p)) < 0
+    assert b"STEPS" in libmpcg.mpcg_last_error()
+    p.steps = 20
+    p.w_v = -1
+    assert libmpcg.mpcg_params_check(C.byref(p)) < 0
+
+
+def test_workspace_bytes(libmpcg):
+    from mpc_ros_amd import _lib
+
+    p = _lib.MpcgParams()
+    libmpcg.mpcg_params_plugin_default(C.byref(p))
+    b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
+    assert b1 > 0 and libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) == 65536 * b1
+    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
+
+
+def test_create_without_gpu_fails_loudly(libmpcg):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    rc = libmpcg.mpcg_create(0, C.byref(h))
+    assert rc < 0 and not h.value
+    assert libmpcg.mpcg_last_error()
+
+
+def test_product_refuses_to_run_without_gpu():
+    """No CPU fallback anywhere in the product: solver construction raises."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from mpc_ros_amd import _lib
+    from mpc_ros_amd.solver import BatchSolver
+
+    with pytest.raises(_lib.MpcgError):
+        BatchSolver(0)
+
+
+def test_product_package_never_imports_oracle():
+    """The product (mpc_ros_amd/) never imports, includes or links the oracle."""
+    pkg = os.path.join(ROOT, "mpc_ros_amd")
+    bad = re.compile(r"(^\s*(import|from)\s+oracle\b|pyoracle|liboracle|#\s*include\s*[\"<][^\">]*ora\.h)", re.M)
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert not bad.search(txt), f

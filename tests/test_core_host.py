@@ -1,0 +1,58 @@
+"""Algorithm check of the device solver core on the CPU (no GPU needed).
+
+tests/native/ipm_host_check.cpp compiles mpc_ros_amd/csrc/ipm_core.h -- the exact
+code the HIP kernel runs per lane -- for the host, into a temporary directory (it is
+never part of the product).  Its results must equal the oracle's fixtures: the
+structured Riccati IPM follows the dense Ipopt restatement iterate for iterate.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, params_from_array
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("hc") / "ipm_host_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-w", "-o", exe,
+                           os.path.join(ROOT, "tests", "native", "ipm_host_check.cpp")])
+    return exe
+
+
+def run_harness(exe, P, state, coeffs, tol=1e-8, max_iter=3000):
+    N = int(P["STEPS"])
+    hdr = (f"{N} {P['DT']!r} {P['REF_CTE']!r} {P['REF_ETHETA']!r} {P['REF_V']!r} {P['W_CTE']!r} {P['W_EPSI']!r} "
+           f"{P['W_V']!r} {P['W_ANGVEL']!r} {P['W_A']!r} {P['W_DANGVEL']!r} {P['W_DA']!r} {P['ANGVEL']!r} "
+           f"{P['MAXTHR']!r} {P['BOUND']!r} {tol!r} {max_iter}\n{len(state)}\n")
+    body = "\n".join(" ".join(repr(float(v)) for v in np.concatenate([state[b], coeffs[b]]))
+                     for b in range(len(state)))
+    out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True).stdout
+    rows = np.array([r.split() for r in out.strip().split("\n")], dtype=np.float64)
+    return dict(status=rows[:, 0].astype(int), iters=rows[:, 1].astype(int), obj=rows[:, 2], u0=rows[:, 3:5],
+                traj=rows[:, 5:].reshape(len(state), 3, N))
+
+
+def compare(r, g, atol=1e-9):
+    np.testing.assert_array_equal(r["status"], g["status"])
+    np.testing.assert_array_equal(r["iters"], g["iters"])
+    np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=atol)
+    np.testing.assert_allclose(r["traj"], g["traj"], rtol=0, atol=atol)
+    np.testing.assert_allclose(r["obj"], g["obj"], rtol=1e-10, atol=1e-9)
+
+
+def test_core_matches_oracle_infinity_set(harness, infinity_golden):
+    g = infinity_golden
+    r = run_harness(harness, params_from_array(g["params"]), g["state"], g["coeffs"])
+    compare(r, g)
+
+
+@pytest.mark.parametrize("name", ["class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound"])
+def test_core_matches_oracle_variants(harness, variants_golden, name):
+    g = variants_golden[name]
+    r = run_harness(harness, params_from_array(g["params"]), g["state"], g["coeffs"])
+    compare(r, g)

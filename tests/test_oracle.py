@@ -1,0 +1,116 @@
+"""The oracle itself: pinned against the reference's known answer and the
+reference's own AD library, and self-consistent with the committed fixtures."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_npz, params_from_array
+
+
+def test_ldlt_solve_and_inertia(oracle):
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        n = int(rng.integers(2, 40))
+        A = rng.standard_normal((n, n))
+        A = A + A.T
+        z = int(rng.integers(0, n // 2 + 1))
+        A[:z, :z] = 0.0
+        ev = np.linalg.eigvalsh(A)
+        if np.min(np.abs(ev)) < 1e-6 * np.max(np.abs(ev)):
+            continue
+        fac, ipiv, inertia = oracle.ldlt(A)
+        b = rng.standard_normal(n)
+        x = oracle.ldlt_solve(fac, ipiv, b)
+        assert np.abs(A @ x - b).max() <= 1e-9 * (1 + np.abs(x).max())
+        assert inertia == (int((ev > 0).sum()), int((ev < 0).sum()), 0)
+
+
+def test_hs071_known_answer(oracle):
+    """The reference's only known-answer test (assets/document/example/CppAD_Ipopt.cpp:146-150)."""
+    with open(os.path.join(GOLDEN, "hs071.json")) as f:
+        ka = json.load(f)
+    r = oracle.hs071()
+    assert r["status"] == 1
+    for key in ("x", "zl", "zu"):
+        np.testing.assert_allclose(r[key], ka[key], rtol=ka["rel_tol"], atol=ka["abs_tol"])
+    assert r["iters"] == 8  # Ipopt's own HS071 iteration count
+
+
+@pytest.mark.parametrize("N", [6, 20])
+def test_nlp_derivatives_match_reference_cppad(oracle, N):
+    """f, g, grad f, J_g and the Lagrangian Hessian of the restated FG_eval equal the
+    values the reference's vendored CppAD computes for the same NLP."""
+    z = load_npz("cppad_derivs.npz")
+    P = params_from_array(z[f"N{N}_params"])
+    for k in range(z[f"N{N}_x"].shape[0]):
+        c, x = z[f"N{N}_coeffs"][k], z[f"N{N}_x"][k]
+        sig, lam = z[f"N{N}_sigma"][k], z[f"N{N}_lambda"][k]
+        fg = oracle.mpc_fg(P, c, x)
+        np.testing.assert_allclose(fg, z[f"N{N}_fg"][k], rtol=1e-13, atol=1e-11)
+        gf, J, H = oracle.mpc_derivs(P, c, x, 1.0, np.zeros(6 * N))
+        np.testing.assert_allclose(gf, z[f"N{N}_jac"][k][0], rtol=1e-13, atol=1e-11)
+        np.testing.assert_allclose(J, z[f"N{N}_jac"][k][1:], rtol=1e-13, atol=1e-11)
+        # CppAD's Hessian weight vector is [sigma, lambda] (fg[0] is the objective)
+        _, _, H = oracle.mpc_derivs(P, c, x, sig, lam)
+        np.testing.assert_allclose(H, z[f"N{N}_hess"][k], rtol=1e-12, atol=1e-9)
+
+
+def test_oracle_reproduces_fixtures(oracle, infinity_golden):
+    g = infinity_golden
+    P = params_from_array(g["params"])
+    sel = np.r_[0:24, 256:264]
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ipm_opts(tol=1e-8))
+    np.testing.assert_array_equal(r["status"], g["status"][sel])
+    np.testing.assert_array_equal(r["iters"], g["iters"][sel])
+    np.testing.assert_allclose(r["u0"], g["u0"][sel], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(r["traj"], g["traj"][sel], rtol=0, atol=1e-12)
+
+
+def test_golden_solutions_are_kkt_points(oracle, infinity_golden):
+    """Independent first-order certificate of the committed solutions."""
+    g = infinity_golden
+    P = params_from_array(g["params"])
+    N = P["STEPS"]
+    for b in range(0, 288, 9):
+        if g["status"][b] != 1:
+            continue
+        # rebuild the full primal vector from the trajectory by integrating the dynamics
+        x = full_primal(oracle, P, g["state"][b], g["coeffs"][b], g["traj"][b], g["u0"][b])
+        if x is None:
+            continue
+        res = oracle.mpc_kkt_residual(P, g["state"][b], g["coeffs"][b], x)
+        assert res["primal"] < 1e-8 and res["bound"] <= 1e-12
+
+
+def full_primal(oracle, P, state, coeffs, traj, u0):
+    r = oracle.mpc_solve(P, state, coeffs, opts=oracle.ipm_opts(tol=1e-8), full=True)
+    if np.abs(r["traj"] - traj).max() > 1e-12:
+        return None
+    return r["x"]
+
+
+def test_oracle_tight_tolerance_converges(oracle, infinity_golden):
+    """At tol 1e-12 the oracle converges to the same local solution as at Ipopt's 1e-8."""
+    g = infinity_golden
+    P = params_from_array(g["params"])
+    sel = np.arange(0, 64, 4)
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ipm_opts(tol=1e-12))
+    ok = (g["status"][sel] == 1) & (r["status"] == 1)
+    assert np.abs(r["u0"][ok] - g["u0"][sel][ok]).max() < 1e-6
+
+
+def test_preprocess_restatement(oracle):
+    z = load_npz("preprocess.npz")
+    for b in range(z["pose"].shape[0]):
+        px, py, yaw = z["pose"][b]
+        v, w, a = z["vel"][b]
+        rc, st, cf = oracle.find_best_path(px, py, yaw, v, w, a, float(z["dt"]), z["plan"][b], True)
+        assert rc == 0
+        np.testing.assert_allclose(st, z["state"][b], atol=1e-13)
+        np.testing.assert_allclose(cf, z["coeffs"][b], atol=1e-13)
+    rc, _, _ = oracle.find_best_path(0, 0, 0, 0, 0, 0, 0.1, np.zeros((0, 2)), True)
+    assert rc == -1  # empty plan (driving_state.cpp:182-185)
