@@ -100,7 +100,7 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
                double* traj, int32_t* status, double* obj, int32_t* iters);
 
 /* Batched solve on device-resident buffers (same layouts), asynchronous on `stream`
- * (a hipStream_t; NULL = the handle's own stream).  No host synchronisation, no
+ * (a hipStream_t; NULL = the null stream, as everywhere in HIP).  No host synchronisation, no
  * allocation if mpcg_reserve(h, B) was called: safe to capture in a HIP graph. */
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);

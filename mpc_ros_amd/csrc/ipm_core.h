@@ -184,25 +184,41 @@ MPCG_HD constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j :
 
 template <typename T, class WS>
 struct IpmSolver {
-    const IpmParams& P;
-    const IpmProblem<T>& pr;
-    WS& ws;
+    // held by value: a reference member would force the kernel-argument structs into
+    // private (scratch) memory and turn every workspace access into a flat access
+    const IpmParams P;
+    const IpmProblem<T> pr;
+    WS ws;
     IpmLayout L;
     int N;
     T dt;
     T sl, su, wl, wu, al, au;        // relaxed bounds: states, angvel, accel
     T sl0, su0, wl0, wu0, al0, au0;  // original bounds
     T sf;                            // objective scale
-    T rs0[6], rs1[6];                // row scales: dynamics rows into stage 1 / into stages >= 2
+    // row scales of the dynamics rows into stage 1 (a*) and into stages >= 2 (b*), as scalars:
+    // an array member selected by stage would become a dynamic address and keep the
+    // whole solver object out of registers
+    T ra0, ra1, ra2, ra3, ra4, ra5, rb0, rb1, rb2, rb3, rb4, rb5;
     T mu, tau;
     // statistics of the current iterate (pass A)
     T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
     int nfilter;
 
-    MPCG_HD IpmSolver(const IpmParams& P_, const IpmProblem<T>& pr_, WS& ws_)
+    MPCG_HD IpmSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WS& ws_)
         : P(P_), pr(pr_), ws(ws_), L{P_.N}, N(P_.N), dt((T)P_.dt) {}
 
-    MPCG_HD T rowscale(int s, int k) const { return k == 0 ? (T)1 : (k == 1 ? rs0[s] : rs1[s]); }
+    MPCG_HD T rowscale(int s, int k) const {
+        T a, b;
+        switch (s) {
+            case 0: a = ra0; b = rb0; break;
+            case 1: a = ra1; b = rb1; break;
+            case 2: a = ra2; b = rb2; break;
+            case 3: a = ra3; b = rb3; break;
+            case 4: a = ra4; b = rb4; break;
+            default: a = ra5; b = rb5; break;
+        }
+        return k == 0 ? (T)1 : (k == 1 ? a : b);
+    }
     MPCG_HD T clo(int j) const { return j == 0 ? wl : al; }
     MPCG_HD T chi(int j) const { return j == 0 ? wu : au; }
 
@@ -282,9 +298,12 @@ struct IpmSolver {
         }
         sf = gm > (T)100 ? (T)100 / gm : (T)1;
         const T u0[2] = {0, 0};
-        rowscales_at(pr.init, u0, rs0);
+        T r[6];
+        rowscales_at(pr.init, u0, r);
+        ra0 = r[0]; ra1 = r[1]; ra2 = r[2]; ra3 = r[3]; ra4 = r[4]; ra5 = r[5];
         const T z6[6] = {0, 0, 0, 0, 0, 0};
-        rowscales_at(z6, u0, rs1);
+        rowscales_at(z6, u0, r);
+        rb0 = r[0]; rb1 = r[1]; rb2 = r[2]; rb3 = r[3]; rb4 = r[4]; rb5 = r[5];
     }
 
     MPCG_HD T push(T v, T lo, T hi) const {
@@ -512,8 +531,8 @@ struct IpmSolver {
                     r[j] = sf * gu[j] - ws[L.ZL(i)] + ws[L.ZU(i)];
                 }
             }
-            // PA = P' A_hat : nonzero columns 0,1,2,3,5 (rows 0..7)
-            T PA[8][5];
+            // PA = P' A_hat : nonzero columns 0,1,2,3,5 (rows 0..7); PB = P' B_hat; h = P' d_hat + p'
+            T PA[8][5], PB[8][2], h[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const T p0 = Pm[pidx(i, 0)], p1 = Pm[pidx(i, 1)], p2 = Pm[pidx(i, 2)];
@@ -523,35 +542,23 @@ struct IpmSolver {
                 PA[i][2] = a[0] * p0 + a[2] * p1 + p2;
                 PA[i][3] = a[1] * p0 + a[3] * p1 + p3 + a[5] * p4;
                 PA[i][4] = a[6] * p4 + p5;  // column 5 (eth)
-            }
-            // PB = P' B_hat (B_hat: w -> dt e2 + dt e5 + e6 ; a -> dt e3 + e7)
-            T PB[8][2];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                PB[i][0] = dt * (Pm[pidx(i, 2)] + Pm[pidx(i, 5)]) + Pm[pidx(i, 6)];
-                PB[i][1] = dt * Pm[pidx(i, 3)] + Pm[pidx(i, 7)];
-            }
-            // h = P' d_hat + p'
-            T h[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                T acc = pv[i];
-#pragma unroll
-                for (int j = 0; j < 6; ++j) acc += Pm[pidx(i, j)] * d[j];
-                h[i] = acc;
+                // B_hat: w -> dt e2 + dt e5 + e6 ; a -> dt e3 + e7
+                PB[i][0] = dt * (p2 + p5) + Pm[pidx(i, 6)];
+                PB[i][1] = dt * p3 + Pm[pidx(i, 7)];
+                h[i] = pv[i] + p0 * d[0] + p1 * d[1] + p2 * d[2] + p3 * d[3] + p4 * d[4] + p5 * d[5];
             }
             const T Rt00 = R0 + dt * (PB[2][0] + PB[5][0]) + PB[6][0];
             const T Rt01 = dt * (PB[2][1] + PB[5][1]) + PB[6][1];
             const T Rt11 = R1 + dt * PB[3][1] + PB[7][1];
             const T det = Rt00 * Rt11 - Rt01 * Rt01;
             if (!(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11)) return false;
-            // S_tilde (2 x 8): columns 0,1,2,3,5 from B^T P A ; 6,7 coupling ; 4 zero
+            // S_tilde (2 x 8): columns 0,1,2,3,5 from B^T P A ; 6,7 the rate coupling ; 4 zero
             T St[2][8];
-            const int cm[5] = {0, 1, 2, 3, 5};
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
-                St[0][cm[c]] = dt * (PA[2][c] + PA[5][c]) + PA[6][c];
-                St[1][cm[c]] = dt * PA[3][c] + PA[7][c];
+                const int col = c < 4 ? c : 5;
+                St[0][col] = dt * (PA[2][c] + PA[5][c]) + PA[6][c];
+                St[1][col] = dt * PA[3][c] + PA[7][c];
             }
             St[0][4] = 0; St[1][4] = 0;
             St[0][6] = C0; St[0][7] = 0;
@@ -567,41 +574,33 @@ struct IpmSolver {
             }
             const T kf0 = -(i00 * rt0 + i01 * rt1);
             const T kf1 = -(i01 * rt0 + i11 * rt1);
-            // P_new = Q_hat + A^T P A + St^T K ; p_new = q_hat + A^T h + St^T kff
-            T AtPA[8][8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                // column c of (P A) in full 8-col indexing
-                T col[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    col[i] = (c == 4 || c >= 6) ? (T)0 : PA[i][c == 5 ? 4 : c];
-                }
-                AtPA[0][c] = col[0] + a[4] * col[4];
-                AtPA[1][c] = col[1] - col[4];
-                AtPA[2][c] = a[0] * col[0] + a[2] * col[1] + col[2];
-                AtPA[3][c] = a[1] * col[0] + a[3] * col[1] + col[3] + a[5] * col[4];
-                AtPA[4][c] = 0;
-                AtPA[5][c] = a[6] * col[4] + col[5];
-                AtPA[6][c] = 0;
-                AtPA[7][c] = 0;
-            }
-            T Pn[36];
+            // P_new = Q_hat + A^T (P A) + St^T K, entry by entry into the (now dead) P registers
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
 #pragma unroll
                 for (int j = 0; j <= i; ++j) {
+                    T atpa = 0;
+                    if (j < 4 || j == 5) {
+                        const int c = j < 4 ? j : 4;
+                        switch (i) {
+                            case 0: atpa = PA[0][c] + a[4] * PA[4][c]; break;
+                            case 1: atpa = PA[1][c] - PA[4][c]; break;
+                            case 2: atpa = a[0] * PA[0][c] + a[2] * PA[1][c] + PA[2][c]; break;
+                            case 3: atpa = a[1] * PA[0][c] + a[3] * PA[1][c] + PA[3][c] + a[5] * PA[4][c]; break;
+                            case 5: atpa = a[6] * PA[4][c] + PA[5][c]; break;
+                            default: atpa = 0;
+                        }
+                    }
                     const T qv = (i < 6 && j < 6) ? Q[pidx(i, j)] : (T)0;
-                    Pn[pidx(i, j)] = qv + AtPA[i][j] + St[0][i] * K[0][j] + St[1][i] * K[1][j];
+                    Pm[pidx(i, j)] = qv + atpa + St[0][i] * K[0][j] + St[1][i] * K[1][j];
                 }
             }
             T At_h[6];
             AT_mul(a, h, At_h);
-            T pn[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const T base = (i < 6) ? q[i] + At_h[i] : (T)0;
-                pn[i] = base + St[0][i] * kf0 + St[1][i] * kf1;
+                pv[i] = base + St[0][i] * kf0 + St[1][i] * kf1;
             }
             // store the record of stage k
 #pragma unroll
@@ -612,17 +611,13 @@ struct IpmSolver {
             ws[L.ST(k, IpmLayout::RKFF)] = kf0;
             ws[L.ST(k, IpmLayout::RKFF + 1)] = kf1;
 #pragma unroll
-            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pn[i];
+            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pm[i];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pn[i];
+            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pv[i];
 #pragma unroll
             for (int i = 0; i < 7; ++i) ws[L.ST(k, IpmLayout::RA + i)] = a[i];
 #pragma unroll
             for (int i = 0; i < 6; ++i) ws[L.ST(k, IpmLayout::RD + i)] = d[i];
-#pragma unroll
-            for (int i = 0; i < 36; ++i) Pm[i] = Pn[i];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) pv[i] = pn[i];
             unext[0] = u[0]; unext[1] = u[1];
             if (k >= 1) { up[0] = um[0]; up[1] = um[1]; }
         }
@@ -778,31 +773,55 @@ struct IpmSolver {
         return ok && isfinite((double)*phi);
     }
 
-    MPCG_HD void accept(T alpha, T amax_z) {
+    // one primal variable and its bound multipliers: z step at the old point, then
+    // z safeguard at the new point (kappa_sigma 1e10)
+    MPCG_HD void accept_var(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun) const {
         const T ksig = (T)1e10;
-        const int nx = L.nx();
-        for (int i = 0; i < nx; ++i) {
-            T lo, hi;
-            if (i < 6 * N) { lo = sl; hi = su; }
-            else if (i < 7 * N - 1) { lo = wl; hi = wu; }
-            else { lo = al; hi = au; }
-            const T w = ws[L.W(i)], dwv = ws[L.DW(i)], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
-            const T dl = w - lo, du = hi - w;
-            const T dzl = mu / dl - zl - zl / dl * dwv;
-            const T dzu = mu / du - zu + zu / du * dwv;
-            const T wn = w + alpha * dwv;
-            const T sl2 = wn - lo, su2 = hi - wn;
-            T zln = zl + amax_z * dzl, zun = zu + amax_z * dzu;
-            zln = tmax(tmin(zln, ksig * mu / sl2), mu / (ksig * sl2));
-            zun = tmax(tmin(zun, ksig * mu / su2), mu / (ksig * su2));
-            ws[L.W(i)] = wn;
-            ws[L.ZL(i)] = zln;
-            ws[L.ZU(i)] = zun;
-        }
-        const int ng = L.ng();
-        for (int r = 0; r < ng; ++r) {
-            const T y = ws[L.Y(r)];
-            ws[L.Y(r)] = y + alpha * (ws[L.YP(r)] - y);
+        const T dl = w - lo, du = hi - w;
+        const T dzl = mu / dl - zl - zl / dl * dwv;
+        const T dzu = mu / du - zu + zu / du * dwv;
+        *wn = w + alpha * dwv;
+        const T sl2 = *wn - lo, su2 = hi - *wn;
+        T a = zl + amax_z * dzl, b = zu + amax_z * dzu;
+        *zln = tmax(tmin(a, ksig * mu / sl2), mu / (ksig * sl2));
+        *zun = tmax(tmin(b, ksig * mu / su2), mu / (ksig * su2));
+    }
+
+    // Stage by stage: all loads of a stage first, then the arithmetic, then the stores.
+    MPCG_HD void accept(T alpha, T amax_z) {
+        for (int k = 0; k < N; ++k) {
+            T w[8], dw[8], zl[8], zu[8], y[6], yp[6];
+            const int nv = (k < N - 1) ? 8 : 6;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const int i = j < 6 ? L.vs(j, k) : L.vu(j - 6, k);
+                    w[j] = ws[L.W(i)];
+                    dw[j] = ws[L.DW(i)];
+                    zl[j] = ws[L.ZL(i)];
+                    zu[j] = ws[L.ZU(i)];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                y[j] = ws[L.Y(L.row(j, k))];
+                yp[j] = ws[L.YP(L.row(j, k))];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T lo = j < 6 ? sl : (j == 6 ? wl : al);
+                    const T hi = j < 6 ? su : (j == 6 ? wu : au);
+                    T wn, zln, zun;
+                    accept_var(w[j], dw[j], zl[j], zu[j], lo, hi, alpha, amax_z, &wn, &zln, &zun);
+                    const int i = j < 6 ? L.vs(j, k) : L.vu(j - 6, k);
+                    ws[L.W(i)] = wn;
+                    ws[L.ZL(i)] = zln;
+                    ws[L.ZU(i)] = zun;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) ws[L.Y(L.row(j, k))] = y[j] + alpha * (yp[j] - y[j]);
         }
     }
 
@@ -946,27 +965,24 @@ struct IpmSolver {
     }
 
     // Final point with honor_original_bounds projection; objective at that point.
-    MPCG_HD T x_out(int i) const {
-        T v = ws[L.W(i)];
-        T lo, hi;
-        if (i < 6 * N) { lo = sl0; hi = su0; }
-        else if (i < 7 * N - 1) { lo = wl0; hi = wu0; }
-        else { lo = al0; hi = au0; }
-        return tmin(tmax(v, lo), hi);
+    MPCG_HD T x_state(int j, int k) const { return tmin(tmax((T)ws[L.W(L.vs(j, k))], sl0), su0); }
+    MPCG_HD T x_ctrl(int j, int k) const {
+        const T v = ws[L.W(L.vu(j, k))];
+        return j == 0 ? tmin(tmax(v, wl0), wu0) : tmin(tmax(v, al0), au0);
     }
     MPCG_HD T objective_out() const {
         T f = 0;
         for (int k = 0; k < N; ++k) {
             T s[6];
 #pragma unroll
-            for (int j = 0; j < 6; ++j) s[j] = x_out(L.vs(j, k));
+            for (int j = 0; j < 6; ++j) s[j] = x_state(j, k);
             f += cost_state(s);
         }
         for (int k = 0; k < N - 1; ++k) {
-            const T w = x_out(L.vu(0, k)), a = x_out(L.vu(1, k));
+            const T w = x_ctrl(0, k), a = x_ctrl(1, k);
             f += (T)P.w_w * w * w + (T)P.w_a * a * a;
             if (k <= N - 3) {
-                const T w1 = x_out(L.vu(0, k + 1)), a1 = x_out(L.vu(1, k + 1));
+                const T w1 = x_ctrl(0, k + 1), a1 = x_ctrl(1, k + 1);
                 f += (T)P.w_dw * (w1 - w) * (w1 - w) + (T)P.w_da * (a1 - a) * (a1 - a);
             }
         }

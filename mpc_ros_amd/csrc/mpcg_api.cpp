@@ -217,7 +217,7 @@ static int ensure_ws(mpcg_handle* h, int64_t B) {
     if (need <= h->ws_bytes) return 0;
     hipSetDevice(h->device);
     if (h->ws) {
-        hipStreamSynchronize(h->stream);
+        hipDeviceSynchronize();  // the old workspace may be in use on any stream
         hipFree(h->ws);
         h->ws = nullptr;
         h->ws_bytes = 0;
@@ -246,7 +246,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     rc = ensure_ws(h, B);
     if (rc) return rc;
-    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
     e = mpcg::launch_ipm_solve(to_ipm(h->params), B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,
                                h->ws, s);
     if (e != hipSuccess) return hip_fail(e, "ipm_solve_kernel launch");

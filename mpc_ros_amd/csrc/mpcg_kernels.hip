@@ -15,11 +15,15 @@
 
 namespace mpcg {
 
+// Workspace accessor.  The pointer is typed in the global address space so that
+// every access is a global_load/global_store (vmcnt-ordered, pipelinable), never a
+// flat access (which orders against LDS too and forces full drains).
 template <typename T>
 struct DevWs {
-    T* base;
+    typedef __attribute__((address_space(1))) T gT;
+    gT* base;
     int64_t stride;
-    __device__ __forceinline__ T& operator[](int e) const { return base[(int64_t)e * stride]; }
+    __device__ __forceinline__ gT& operator[](int e) const { return base[(int64_t)e * stride]; }
 };
 
 __global__ void __launch_bounds__(64, 1)
@@ -33,19 +37,18 @@ ipm_solve_kernel(IpmParams P, int64_t B, const double* __restrict__ state, const
     for (int j = 0; j < 6; ++j) pr.init[j] = state[p * 6 + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) pr.c[j] = coeffs[p * 4 + j];
-    DevWs<double> w{ws + p, B};
+    DevWs<double> w{(DevWs<double>::gT*)(ws + p), B};
     IpmSolver<double, DevWs<double>> S(P, pr, w);
     const IpmResult r = S.solve();
-    const IpmLayout L{P.N};
-    u0[p * 2 + 0] = S.x_out(L.vu(0, 0));
-    u0[p * 2 + 1] = S.x_out(L.vu(1, 0));
+    u0[p * 2 + 0] = S.x_ctrl(0, 0);
+    u0[p * 2 + 1] = S.x_ctrl(1, 0);
     if (traj) {
         const int N = P.N;
         double* t = traj + p * 3 * N;
         for (int k = 0; k < N; ++k) {
-            t[k] = S.x_out(L.vs(0, k));
-            t[N + k] = S.x_out(L.vs(1, k));
-            t[2 * N + k] = S.x_out(L.vs(2, k));
+            t[k] = S.x_state(0, k);
+            t[N + k] = S.x_state(1, k);
+            t[2 * N + k] = S.x_state(2, k);
         }
     }
     if (status) status[p] = r.status;

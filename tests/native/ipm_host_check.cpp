@@ -39,10 +39,10 @@ int main() {
         HostWs ws{buf.data()};
         mpcg::IpmSolver<double, HostWs> S(P, pr, ws);
         mpcg::IpmResult r = S.solve();
-        std::printf("%d %d %.17g %.17g %.17g", r.status, r.iters, S.objective_out(), S.x_out(L.vu(0, 0)),
-                    S.x_out(L.vu(1, 0)));
+        std::printf("%d %d %.17g %.17g %.17g", r.status, r.iters, S.objective_out(), S.x_ctrl(0, 0),
+                    S.x_ctrl(1, 0));
         for (int s = 0; s < 3; ++s)
-            for (int k = 0; k < P.N; ++k) std::printf(" %.17g", S.x_out(L.vs(s, k)));
+            for (int k = 0; k < P.N; ++k) std::printf(" %.17g", S.x_state(s, k));
         std::printf("\n");
     }
     return 0;
