@@ -34,6 +34,16 @@
 #else
 #define MPCG_HD inline
 #endif
+// MPCG_NOINLINE_PASSES keeps the four sweeps of an iteration as separate device
+// functions (no spills, but the call overhead measured slower: 606K vs 794K solves/s),
+// so the default inlines them.
+#if defined(__HIPCC__) && defined(MPCG_NOINLINE_PASSES)
+#define MPCG_PASS __host__ __device__ __attribute__((noinline))
+#elif defined(__HIPCC__)
+#define MPCG_PASS MPCG_HD
+#else
+#define MPCG_PASS inline
+#endif
 
 namespace mpcg {
 
@@ -59,27 +69,25 @@ enum : int32_t {
     IPM_INVALID_NUMBER = 11,
 };
 
-// Workspace layout of one problem; element e lives at ws[e * stride].
+// Workspace layout of one problem, in elements (doubles).  Everything is stage-major:
+// stage k's primal block is [x y th v cte eth | w a] (8 elements), likewise its bound
+// multipliers, step, multipliers (6 rows + 2 pad) and Riccati record (80).  The device
+// accessor stores element pairs (2j, 2j+1) of one problem contiguously and pairs of
+// consecutive problems next to each other, so a lane moves 16 B per instruction and
+// a wavefront 1 KB of contiguous memory.
 struct IpmLayout {
     int N;
-    static constexpr int STAGE = 80;  // per-stage Riccati record (75 used)
-    // record offsets
-    static constexpr int RK = 0, RKFF = 16, RP = 18, Rp = 54, RA = 62, RD = 69;
-    MPCG_HD int nx() const { return 8 * N - 2; }
-    MPCG_HD int ng() const { return 6 * N; }
-    MPCG_HD int W(int i) const { return i; }
-    MPCG_HD int ZL(int i) const { return nx() + i; }
-    MPCG_HD int ZU(int i) const { return 2 * nx() + i; }
-    MPCG_HD int DW(int i) const { return 3 * nx() + i; }
-    MPCG_HD int Y(int r) const { return 4 * nx() + r; }
-    MPCG_HD int YP(int r) const { return 4 * nx() + ng() + r; }
-    MPCG_HD int ST(int k, int j) const { return 4 * nx() + 2 * ng() + STAGE * k + j; }
-    MPCG_HD int FI(int j) const { return 4 * nx() + 2 * ng() + STAGE * N + j; }
-    MPCG_HD int total(int cap) const { return 4 * nx() + 2 * ng() + STAGE * N + 2 * cap; }
-    // reference layout (mpc_planner.cpp:252-259)
-    MPCG_HD int vs(int s, int k) const { return s * N + k; }
-    MPCG_HD int vu(int j, int k) const { return 6 * N + j * (N - 1) + k; }
-    MPCG_HD int row(int s, int k) const { return s * N + k; }
+    static constexpr int RS = 80;  // Riccati record: K[16] kff[2] P[36] p[8] A[7]+pad d[6] (+pad)
+    static constexpr int RK = 0, RKFF = 16, RP = 18, Rp = 54, RA = 62, RD = 70;
+    MPCG_HD int W(int k, int j) const { return 8 * k + j; }
+    MPCG_HD int ZL(int k, int j) const { return 8 * N + 8 * k + j; }
+    MPCG_HD int ZU(int k, int j) const { return 16 * N + 8 * k + j; }
+    MPCG_HD int DW(int k, int j) const { return 24 * N + 8 * k + j; }
+    MPCG_HD int Y(int k, int j) const { return 32 * N + 8 * k + j; }
+    MPCG_HD int YP(int k, int j) const { return 40 * N + 8 * k + j; }
+    MPCG_HD int REC(int k, int j) const { return 48 * N + RS * k + j; }
+    MPCG_HD int FI(int j) const { return 128 * N + j; }
+    MPCG_HD int total(int cap) const { return 128 * N + 2 * cap + 2; }
 };
 
 template <typename T>
@@ -109,6 +117,21 @@ template <typename T>
 MPCG_HD T tmax(T a, T b) { return a > b ? a : b; }
 template <typename T>
 MPCG_HD T tmin(T a, T b) { return a < b ? a : b; }
+
+// Reciprocal: on the device v_rcp_f64 refined by two Newton steps (5 instructions,
+// within an ulp of 1/x) instead of the ~10-instruction correctly rounded division;
+// every slack of every variable needs one per sweep.
+MPCG_HD double rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
 
 // Sum of logs accumulated as mantissa * 2^exponent: one log per pass.
 template <typename T>
@@ -182,8 +205,31 @@ MPCG_HD void A_mul(const T* a, const T* x, T* y) {
 
 MPCG_HD constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
+
+// Diagnostic cycle stamps (tools/diag_stamps.hip only; never in the product build).
+#if defined(MPCG_DIAG)
+#define MPCG_STAMP_DECL uint64_t tacc[6] = {0, 0, 0, 0, 0, 0}; uint64_t tlast = 0;
+#endif
+#if defined(MPCG_DIAG) && defined(__HIP_DEVICE_COMPILE__)
+#define MPCG_STAMP_BEGIN() (tlast = __builtin_amdgcn_s_memtime())
+#define MPCG_STAMP(slot) do { uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[slot] += _t - tlast; tlast = _t; } while (0)
+#else
+#if !defined(MPCG_DIAG)
+#define MPCG_STAMP_DECL
+#endif
+#define MPCG_STAMP_BEGIN() ((void)0)
+#define MPCG_STAMP(slot) ((void)0)
+#endif
+
+// One stage's iterate as loaded from the workspace.
+template <typename T>
+struct StageIt {
+    T w[8], dw[8], zl[8], zu[8], y[6], yp[6];
+};
+
 template <typename T, class WS>
 struct IpmSolver {
+    MPCG_STAMP_DECL
     // held by value: a reference member would force the kernel-argument structs into
     // private (scratch) memory and turn every workspace access into a flat access
     const IpmParams P;
@@ -200,12 +246,40 @@ struct IpmSolver {
     // whole solver object out of registers
     T ra0, ra1, ra2, ra3, ra4, ra5, rb0, rb1, rb2, rb3, rb4, rb5;
     T mu, tau;
-    // statistics of the current iterate (pass A)
+    // statistics of the current iterate
     T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
     int nfilter;
 
     MPCG_HD IpmSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WS& ws_)
         : P(P_), pr(pr_), ws(ws_), L{P_.N}, N(P_.N), dt((T)P_.dt) {}
+
+    // -------------------------------------------------------- memory helpers
+    MPCG_HD void ld8(int e, T* v) const {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) ws.ld2(e + j, v[j], v[j + 1]);
+    }
+    MPCG_HD void ld6(int e, T* v) const {
+#pragma unroll
+        for (int j = 0; j < 6; j += 2) ws.ld2(e + j, v[j], v[j + 1]);
+    }
+    MPCG_HD void st8(int e, const T* v) const {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) ws.st2(e + j, v[j], v[j + 1]);
+    }
+    MPCG_HD void st6(int e, const T* v) const {
+#pragma unroll
+        for (int j = 0; j < 6; j += 2) ws.st2(e + j, v[j], v[j + 1]);
+    }
+    MPCG_HD void load_stage(int k, StageIt<T>& S, bool with_dir) const {
+        ld8(L.W(k, 0), S.w);
+        ld8(L.ZL(k, 0), S.zl);
+        ld8(L.ZU(k, 0), S.zu);
+        ld6(L.Y(k, 0), S.y);
+        if (with_dir) {
+            ld8(L.DW(k, 0), S.dw);
+            ld6(L.YP(k, 0), S.yp);
+        }
+    }
 
     MPCG_HD T rowscale(int s, int k) const {
         T a, b;
@@ -219,17 +293,8 @@ struct IpmSolver {
         }
         return k == 0 ? (T)1 : (k == 1 ? a : b);
     }
-    MPCG_HD T clo(int j) const { return j == 0 ? wl : al; }
-    MPCG_HD T chi(int j) const { return j == 0 ? wu : au; }
-
-    MPCG_HD void load_s(int k, T* s) const {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) s[j] = ws[L.W(L.vs(j, k))];
-    }
-    MPCG_HD void load_u(int k, T* u) const {
-        u[0] = ws[L.W(L.vu(0, k))];
-        u[1] = ws[L.W(L.vu(1, k))];
-    }
+    MPCG_HD T vlo(int j) const { return j < 6 ? sl : (j == 6 ? wl : al); }
+    MPCG_HD T vhi(int j) const { return j < 6 ? su : (j == 6 ? wu : au); }
 
     // objective pieces (unscaled) -- FG_eval cost, mpc_planner.cpp:122-147
     MPCG_HD T cost_state(const T* s) const {
@@ -242,7 +307,10 @@ struct IpmSolver {
         g[4] = (T)(2.0 * P.w_cte) * (s[4] - (T)P.ref_cte);
         g[5] = (T)(2.0 * P.w_eth) * (s[5] - (T)P.ref_eth);
     }
-    // gradient w.r.t. u_k given u_{k-1} (valid if k>=1) and u_{k+1} (valid if k<=N-3)
+    MPCG_HD T hess_state(int j) const {
+        return j == 3 ? (T)(2.0 * P.w_v) : (j == 4 ? (T)(2.0 * P.w_cte) : (j == 5 ? (T)(2.0 * P.w_eth) : (T)0));
+    }
+    // gradient w.r.t. u_k given u_{k-1} (used if k>=1) and u_{k+1} (used if k<=N-3)
     MPCG_HD void grad_ctrl(int k, const T* um, const T* u, const T* up, T* g) const {
         g[0] = (T)(2.0 * P.w_w) * u[0];
         g[1] = (T)(2.0 * P.w_a) * u[1];
@@ -260,21 +328,26 @@ struct IpmSolver {
         const double w = j == 0 ? P.w_w : P.w_a;
         return (T)(2.0 * w + 2.0 * wd * ((k >= 1 ? 1 : 0) + (k <= N - 3 ? 1 : 0)));
     }
+    MPCG_HD T cost_ctrl(int k, const T* u, const T* up) const {
+        T f = (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
+        if (k <= N - 3)
+            f += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
+        return f;
+    }
 
     // ------------------------------------------------------------------ setup
     // Bounds of MPC::Solve (mpc_planner.cpp:303-325) relaxed as Ipopt does;
     // gradient-based scaling at the user's starting point; starting point pushed
     // inside the box; bound multipliers 1; least-squares equality multipliers.
-    MPCG_HD void rowscales_at(const T* s, const T* u, T* rs) const {
+    MPCG_HD void rowscales_at(const T* s, T* rs) const {
         Lin<T> ln;
         ln.eval(pr.c, s);
-        (void)u;
         T m[6];
-        m[0] = tmax((T)1, tmax(fabs(s[3] * ln.st * dt), fabs(ln.ct * dt)));
-        m[1] = tmax((T)1, tmax(fabs(s[3] * ln.ct * dt), fabs(ln.st * dt)));
+        m[0] = tmax((T)1, tmax((T)fabs(s[3] * ln.st * dt), (T)fabs(ln.ct * dt)));
+        m[1] = tmax((T)1, tmax((T)fabs(s[3] * ln.ct * dt), (T)fabs(ln.st * dt)));
         m[2] = tmax((T)1, dt);
         m[3] = tmax((T)1, dt);
-        m[4] = tmax(tmax((T)1, fabs(ln.f1)), tmax(fabs(ln.se * dt), fabs(s[3] * ln.ce * dt)));
+        m[4] = tmax(tmax((T)1, (T)fabs(ln.f1)), tmax((T)fabs(ln.se * dt), (T)fabs(s[3] * ln.ce * dt)));
         m[5] = tmax((T)1, dt);
 #pragma unroll
         for (int j = 0; j < 6; ++j) rs[j] = m[j] > (T)100 ? (T)100 / m[j] : (T)1;
@@ -290,19 +363,18 @@ struct IpmSolver {
         // objective scale from grad f at the user start (zeros except s_0)
         T g[6];
         grad_state(pr.init, g);
-        T gm = tmax(fabs(g[3]), tmax(fabs(g[4]), fabs(g[5])));
+        T gm = tmax((T)fabs(g[3]), tmax((T)fabs(g[4]), (T)fabs(g[5])));
         if (N >= 2) {
             const T z[6] = {0, 0, 0, 0, 0, 0};
             grad_state(z, g);
-            gm = tmax(gm, tmax(fabs(g[3]), tmax(fabs(g[4]), fabs(g[5]))));
+            gm = tmax(gm, tmax((T)fabs(g[3]), tmax((T)fabs(g[4]), (T)fabs(g[5]))));
         }
         sf = gm > (T)100 ? (T)100 / gm : (T)1;
-        const T u0[2] = {0, 0};
         T r[6];
-        rowscales_at(pr.init, u0, r);
+        rowscales_at(pr.init, r);
         ra0 = r[0]; ra1 = r[1]; ra2 = r[2]; ra3 = r[3]; ra4 = r[4]; ra5 = r[5];
         const T z6[6] = {0, 0, 0, 0, 0, 0};
-        rowscales_at(z6, u0, r);
+        rowscales_at(z6, r);
         rb0 = r[0]; rb1 = r[1]; rb2 = r[2]; rb3 = r[3]; rb4 = r[4]; rb5 = r[5];
     }
 
@@ -315,107 +387,123 @@ struct IpmSolver {
     }
 
     MPCG_HD void init_point() {
-        for (int k = 0; k < N; ++k)
+        const T one[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+        for (int k = 0; k < N; ++k) {
+            T w[8];
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const int i = L.vs(j, k);
-                ws[L.W(i)] = push(k == 0 ? pr.init[j] : (T)0, sl, su);
-                ws[L.ZL(i)] = 1;
-                ws[L.ZU(i)] = 1;
-            }
-        for (int k = 0; k < N - 1; ++k)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int i = L.vu(j, k);
-                ws[L.W(i)] = push((T)0, clo(j), chi(j));
-                ws[L.ZL(i)] = 1;
-                ws[L.ZU(i)] = 1;
-            }
+            for (int j = 0; j < 8; ++j) w[j] = push((j < 6 && k == 0) ? pr.init[j] : (T)0, vlo(j), vhi(j));
+            st8(L.W(k, 0), w);
+            st8(L.ZL(k, 0), one);
+            st8(L.ZU(k, 0), one);
+        }
     }
 
-    // ---------------------------------------------------------------- pass A
-    // Statistics of the current iterate: objective, barrier log-sum, constraint
-    // violation (l1 and max), dual infeasibility, complementarity extrema, l1 norms.
-    MPCG_HD void stats() {
+    // ------------------------------------------------ accept + statistics
+    // One forward sweep.  If `acc`, first applies the previous line-search step to
+    // stage k (primal w += alpha dw, z step with the fraction-to-boundary alpha_z
+    // and the kappa_sigma safeguard, y += alpha (y+ - y)), then accumulates the
+    // statistics of the new iterate: objective, barrier log-sum, constraint
+    // violation (l1 and max), dual infeasibility, complementarity extrema and norms.
+    // Stage k+1 is loaded one step ahead so its loads overlap stage k's work.
+    MPCG_HD void accept_one(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun) const {
+        const T ksig = (T)1e10, iksig = (T)1e-10;
+        const T rdl = rcp(w - lo), rdu = rcp(hi - w);
+        const T dzl = mu * rdl - zl - zl * rdl * dwv;
+        const T dzu = mu * rdu - zu + zu * rdu * dwv;
+        *wn = w + alpha * dwv;
+        const T rs2 = rcp(*wn - lo), ru2 = rcp(hi - *wn);
+        const T a = zl + amax_z * dzl, b = zu + amax_z * dzu;
+        *zln = tmax(tmin(a, ksig * mu * rs2), mu * rs2 * iksig);
+        *zun = tmax(tmin(b, ksig * mu * ru2), mu * ru2 * iksig);
+    }
+
+    MPCG_PASS void stats(bool acc, T alpha, T amax_z) {
         fval = 0; theta = 0; prim_inf = 0; prim_uns = 0; dual_inf = 0; compl0 = 0;
         pmin = (T)INFINITY; pmax = -(T)INFINITY; l1y = 0; l1z = 0;
         LogAcc<T> la;
         la.init();
-        T Fprev[6], um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
-        if (N >= 2) load_u(0, u);
+        StageIt<T> cur, nxt;
+        load_stage(0, cur, acc);
+        T Fprev[6] = {0, 0, 0, 0, 0, 0};
+        T um[2] = {0, 0};
         for (int k = 0; k < N; ++k) {
-            T s[6];
-            load_s(k, s);
-            const bool hasu = k < N - 1;
-            if (k + 1 < N - 1) load_u(k + 1, up);
-            // residual rows (s, k)
-            T yk[6];
+            const bool last = (k == N - 1);
+            if (!last) load_stage(k + 1, nxt, acc);  // prefetch, ahead of this stage's stores
+            // new iterate of stage k
+            T w[8], zl[8], zu[8], y[6];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (acc && !(last && j >= 6)) {
+                    accept_one(cur.w[j], cur.dw[j], cur.zl[j], cur.zu[j], vlo(j), vhi(j), alpha, amax_z, &w[j], &zl[j],
+                               &zu[j]);
+                } else {
+                    w[j] = cur.w[j]; zl[j] = cur.zl[j]; zu[j] = cur.zu[j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) y[j] = acc ? cur.y[j] + alpha * (cur.yp[j] - cur.y[j]) : cur.y[j];
+            if (acc) {
+                st8(L.W(k, 0), w);
+                st8(L.ZL(k, 0), zl);
+                st8(L.ZU(k, 0), zu);
+                st6(L.Y(k, 0), y);
+            }
+            // new u_{k+1} and y_{k+1} (same formulas as at step k+1)
+            T up[2] = {0, 0}, yn[6] = {0, 0, 0, 0, 0, 0};
+            if (!last) {
+                up[0] = acc ? nxt.w[6] + alpha * nxt.dw[6] : nxt.w[6];
+                up[1] = acc ? nxt.w[7] + alpha * nxt.dw[7] : nxt.w[7];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) yn[j] = acc ? nxt.y[j] + alpha * (nxt.yp[j] - nxt.y[j]) : nxt.y[j];
+            }
+            // residual rows (., k)
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const T c = k == 0 ? s[j] - pr.init[j] : s[j] - Fprev[j];
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
                 const T rsc = rowscale(j, k);
                 const T cs = rsc * c;
                 theta += fabs(cs);
                 prim_inf = tmax(prim_inf, (T)fabs(cs));
                 prim_uns = tmax(prim_uns, (T)fabs(c));
-                yk[j] = ws[L.Y(L.row(j, k))];
-                l1y += fabs(yk[j]) / rsc;
+                l1y += fabs(y[j]) * rcp(rsc);
             }
-            fval += cost_state(s);
-            // dual residual of the states
+            fval += cost_state(w);
             T g[6], at[6] = {0, 0, 0, 0, 0, 0};
-            grad_state(s, g);
-            Lin<T> ln;
-            T a[7];
-            T ynext[6];
-            if (hasu) {
-                ln.eval(pr.c, s);
-                ln.jac(s, dt, a);
-                ln.next(s, u, dt, Fprev);
-#pragma unroll
-                for (int j = 0; j < 6; ++j) ynext[j] = ws[L.Y(L.row(j, k + 1))];
-                AT_mul(a, ynext, at);
+            grad_state(w, g);
+            if (!last) {
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                T a[7];
+                ln.jac(w, dt, a);
+                ln.next(w, w + 6, dt, Fprev);
+                AT_mul(a, yn, at);
             }
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const int i = L.vs(j, k);
-                const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
-                const T rd = sf * g[j] - zl + zu + yk[j] - at[j];
-                dual_inf = tmax(dual_inf, (T)fabs(rd));
-                const T dl = w - sl, du = su - w;
-                la.mul(dl);
-                la.mul(du);
-                const T p1 = dl * zl, p2 = du * zu;
-                compl0 = tmax(compl0, tmax((T)fabs(p1), (T)fabs(p2)));
-                pmin = tmin(pmin, tmin(p1, p2));
-                pmax = tmax(pmax, tmax(p1, p2));
-                l1z += fabs(zl) + fabs(zu);
+            T gu[2] = {0, 0};
+            if (!last) {
+                grad_ctrl(k, um, w + 6, up, gu);
+                fval += cost_ctrl(k, w + 6, up);
             }
-            if (hasu) {
-                T gu[2];
-                grad_ctrl(k, um, u, up, gu);
-                fval += (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
-                if (k <= N - 3)
-                    fval += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
-                const T btw = dt * (ynext[2] + ynext[5]), bta = dt * ynext[3];
+            const T btw = dt * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;  // product of the stage's 16 slacks, inside double range for any iterate
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int i = L.vu(j, k);
-                    const T w = u[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
-                    const T rd = sf * gu[j] - zl + zu - (j == 0 ? btw : bta);
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T gj = j < 6 ? sf * g[j] + y[j] - at[j] : sf * gu[j - 6] - (j == 6 ? btw : bta);
+                    const T rd = gj - zl[j] + zu[j];
                     dual_inf = tmax(dual_inf, (T)fabs(rd));
-                    const T dl = w - clo(j), du = chi(j) - w;
-                    la.mul(dl);
-                    la.mul(du);
-                    const T p1 = dl * zl, p2 = du * zu;
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    slackprod *= dl * du;
+                    const T p1 = dl * zl[j], p2 = du * zu[j];
                     compl0 = tmax(compl0, tmax((T)fabs(p1), (T)fabs(p2)));
                     pmin = tmin(pmin, tmin(p1, p2));
                     pmax = tmax(pmax, tmax(p1, p2));
-                    l1z += fabs(zl) + fabs(zu);
+                    l1z += fabs(zl[j]) + fabs(zu[j]);
                 }
-                um[0] = u[0]; um[1] = u[1];
-                u[0] = up[0]; u[1] = up[1];
             }
+            la.mul(slackprod);
+            um[0] = w[6]; um[1] = w[7];
+            cur = nxt;
         }
         logsum = la.value();
     }
@@ -424,46 +512,62 @@ struct IpmSolver {
     // mode 0: Newton system of the barrier problem (Hessian of the Lagrangian + Sigma + delta_w I)
     // mode 1: least-squares multiplier system (identity Hessian, zero constraint residual)
     // Returns false when a stage's reduced control Hessian is not positive definite.
-    MPCG_HD bool riccati(int mode, T delta_w) {
+    MPCG_PASS bool riccati(int mode, T delta_w) {
         T Pm[36], pv[8];
+        // prefetched stage data: W[k], ZL[k], ZU[k] and Y[k+1]
+        T cw[8], czl[8], czu[8], cy[6];
+        T nw_[8], nzl[8], nzu[8], ny[6];
+        ld8(L.W(N - 1, 0), cw);
+        ld8(L.ZL(N - 1, 0), czl);
+        ld8(L.ZU(N - 1, 0), czu);
+        if (N >= 2) {
+            ld8(L.W(N - 2, 0), nw_);
+            ld8(L.ZL(N - 2, 0), nzl);
+            ld8(L.ZU(N - 2, 0), nzu);
+            ld6(L.Y(N - 1, 0), ny);
+        }
         // terminal stage
         {
-            const int k = N - 1;
-            T s[6];
-            load_s(k, s);
             T g[6];
-            grad_state(s, g);
+            grad_state(cw, g);
 #pragma unroll
             for (int i = 0; i < 36; ++i) Pm[i] = 0;
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const int i = L.vs(j, k);
-                const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
                 if (mode == 0) {
-                    const T dl = w - sl, du = su - w;
-                    const T hd = (j >= 3 ? sf * (T)(2.0 * (j == 3 ? P.w_v : (j == 4 ? P.w_cte : P.w_eth))) : (T)0);
-                    Pm[pidx(j, j)] = hd + zl / dl + zu / du + delta_w;
-                    pv[j] = sf * g[j] - mu / dl + mu / du;
+                    const T rdl = rcp(cw[j] - sl), rdu = rcp(su - cw[j]);
+                    Pm[pidx(j, j)] = sf * hess_state(j) + czl[j] * rdl + czu[j] * rdu + delta_w;
+                    pv[j] = sf * g[j] - mu * rdl + mu * rdu;
                 } else {
                     Pm[pidx(j, j)] = 1;
-                    pv[j] = sf * g[j] - zl + zu;
+                    pv[j] = sf * g[j] - czl[j] + czu[j];
                 }
             }
             pv[6] = 0; pv[7] = 0;
 #pragma unroll
-            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pm[i];
+            for (int i = 0; i < 36; i += 2) ws.st2(L.REC(N - 1, IpmLayout::RP + i), Pm[i], Pm[i + 1]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pv[i];
+            for (int i = 0; i < 8; i += 2) ws.st2(L.REC(N - 1, IpmLayout::Rp + i), pv[i], pv[i + 1]);
         }
-        T up[2] = {0, 0};
-        if (N >= 2) load_u(N - 2, up);  // u_{k} for k = N-2 at loop start
+        T snext[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) snext[j] = cw[j];
         T unext[2] = {0, 0};
         for (int k = N - 2; k >= 0; --k) {
-            T s[6], u[2], um[2] = {0, 0}, snext[6];
-            load_s(k, s);
-            u[0] = up[0]; u[1] = up[1];
-            if (k >= 1) load_u(k - 1, um);
-            load_s(k + 1, snext);
+            // rotate the prefetch buffers: stage k becomes current
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { cw[j] = nw_[j]; czl[j] = nzl[j]; czu[j] = nzu[j]; }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) cy[j] = ny[j];
+            if (k >= 1) {  // prefetch stage k-1 before this stage's stores
+                ld8(L.W(k - 1, 0), nw_);
+                ld8(L.ZL(k - 1, 0), nzl);
+                ld8(L.ZU(k - 1, 0), nzu);
+                ld6(L.Y(k, 0), ny);
+            }
+            const T* s = cw;
+            const T u[2] = {cw[6], cw[7]};
+            const T um[2] = {k >= 1 ? nw_[6] : (T)0, k >= 1 ? nw_[7] : (T)0};
             Lin<T> ln;
             ln.eval(pr.c, s);
             T a[7];
@@ -471,12 +575,8 @@ struct IpmSolver {
             T Fk[6];
             ln.next(s, u, dt, Fk);
             T d[6];
-            T yn[6];
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                d[j] = (mode == 0) ? Fk[j] - snext[j] : (T)0;
-                yn[j] = ws[L.Y(L.row(j, k + 1))];
-            }
+            for (int j = 0; j < 6; ++j) d[j] = (mode == 0) ? Fk[j] - snext[j] : (T)0;
             // stage Hessian Q (6x6, packed), R diag, coupling C, gradients q, r
             T Q[21];
 #pragma unroll
@@ -489,28 +589,23 @@ struct IpmSolver {
             if (mode == 0) {
 #pragma unroll
                 for (int j = 0; j < 6; ++j) {
-                    const int i = L.vs(j, k);
-                    const T w = s[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
-                    const T dl = w - sl, du = su - w;
-                    const T hd = (j >= 3 ? sf * (T)(2.0 * (j == 3 ? P.w_v : (j == 4 ? P.w_cte : P.w_eth))) : (T)0);
-                    Q[pidx(j, j)] = hd + zl / dl + zu / du + delta_w;
-                    q[j] = sf * g[j] - mu / dl + mu / du;
+                    const T rdl = rcp(s[j] - sl), rdu = rcp(su - s[j]);
+                    Q[pidx(j, j)] = sf * hess_state(j) + czl[j] * rdl + czu[j] * rdu + delta_w;
+                    q[j] = sf * g[j] - mu * rdl + mu * rdu;
                 }
                 // constraint curvature, weighted by the row-form multipliers of rows k+1
                 const T v = s[3];
-                Q[pidx(2, 2)] += yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;
-                Q[pidx(3, 2)] += yn[0] * ln.st * dt - yn[1] * ln.ct * dt;
-                Q[pidx(0, 0)] += -yn[4] * ln.f2;
-                Q[pidx(5, 5)] += yn[4] * v * ln.se * dt;
-                Q[pidx(5, 3)] += -yn[4] * ln.ce * dt;
+                Q[pidx(2, 2)] += cy[0] * v * ln.ct * dt + cy[1] * v * ln.st * dt;
+                Q[pidx(3, 2)] += cy[0] * ln.st * dt - cy[1] * ln.ct * dt;
+                Q[pidx(0, 0)] += -cy[4] * ln.f2;
+                Q[pidx(5, 5)] += cy[4] * v * ln.se * dt;
+                Q[pidx(5, 3)] += -cy[4] * ln.ce * dt;
                 T Rr[2];
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const int i = L.vu(j, k);
-                    const T w = u[j], zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
-                    const T dl = w - clo(j), du = chi(j) - w;
-                    Rr[j] = sf * hess_ctrl(k, j) + zl / dl + zu / du + delta_w;
-                    r[j] = sf * gu[j] - mu / dl + mu / du;
+                    const T rdl = rcp(u[j] - vlo(6 + j)), rdu = rcp(vhi(6 + j) - u[j]);
+                    Rr[j] = sf * hess_ctrl(k, j) + czl[6 + j] * rdl + czu[6 + j] * rdu + delta_w;
+                    r[j] = sf * gu[j] - mu * rdl + mu * rdu;
                 }
                 R0 = Rr[0]; R1 = Rr[1];
                 if (k >= 1) {
@@ -520,16 +615,12 @@ struct IpmSolver {
             } else {
 #pragma unroll
                 for (int j = 0; j < 6; ++j) {
-                    const int i = L.vs(j, k);
                     Q[pidx(j, j)] = 1;
-                    q[j] = sf * g[j] - ws[L.ZL(i)] + ws[L.ZU(i)];
+                    q[j] = sf * g[j] - czl[j] + czu[j];
                 }
                 R0 = 1; R1 = 1;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int i = L.vu(j, k);
-                    r[j] = sf * gu[j] - ws[L.ZL(i)] + ws[L.ZU(i)];
-                }
+                for (int j = 0; j < 2; ++j) r[j] = sf * gu[j] - czl[6 + j] + czu[6 + j];
             }
             // PA = P' A_hat : nonzero columns 0,1,2,3,5 (rows 0..7); PB = P' B_hat; h = P' d_hat + p'
             T PA[8][5], PB[8][2], h[8];
@@ -565,7 +656,8 @@ struct IpmSolver {
             St[1][6] = 0;  St[1][7] = C1;
             const T rt0 = r[0] + dt * (h[2] + h[5]) + h[6];
             const T rt1 = r[1] + dt * h[3] + h[7];
-            const T i00 = Rt11 / det, i01 = -Rt01 / det, i11 = Rt00 / det;
+            const T rdet = rcp(det);
+            const T i00 = Rt11 * rdet, i01 = -Rt01 * rdet, i11 = Rt00 * rdet;
             T K[2][8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -602,227 +694,196 @@ struct IpmSolver {
                 const T base = (i < 6) ? q[i] + At_h[i] : (T)0;
                 pv[i] = base + St[0][i] * kf0 + St[1][i] * kf1;
             }
-            // store the record of stage k
+            // record of stage k (pair stores)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                ws[L.ST(k, IpmLayout::RK + j)] = K[0][j];
-                ws[L.ST(k, IpmLayout::RK + 8 + j)] = K[1][j];
+            for (int j = 0; j < 8; j += 2) {
+                ws.st2(L.REC(k, IpmLayout::RK + j), K[0][j], K[0][j + 1]);
+                ws.st2(L.REC(k, IpmLayout::RK + 8 + j), K[1][j], K[1][j + 1]);
             }
-            ws[L.ST(k, IpmLayout::RKFF)] = kf0;
-            ws[L.ST(k, IpmLayout::RKFF + 1)] = kf1;
+            ws.st2(L.REC(k, IpmLayout::RKFF), kf0, kf1);
 #pragma unroll
-            for (int i = 0; i < 36; ++i) ws[L.ST(k, IpmLayout::RP + i)] = Pm[i];
+            for (int i = 0; i < 36; i += 2) ws.st2(L.REC(k, IpmLayout::RP + i), Pm[i], Pm[i + 1]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ws[L.ST(k, IpmLayout::Rp + i)] = pv[i];
+            for (int i = 0; i < 8; i += 2) ws.st2(L.REC(k, IpmLayout::Rp + i), pv[i], pv[i + 1]);
+            ws.st2(L.REC(k, IpmLayout::RA + 0), a[0], a[1]);
+            ws.st2(L.REC(k, IpmLayout::RA + 2), a[2], a[3]);
+            ws.st2(L.REC(k, IpmLayout::RA + 4), a[4], a[5]);
+            ws.st2(L.REC(k, IpmLayout::RA + 6), a[6], (T)0);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) ws[L.ST(k, IpmLayout::RA + i)] = a[i];
+            for (int i = 0; i < 6; i += 2) ws.st2(L.REC(k, IpmLayout::RD + i), d[i], d[i + 1]);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) ws[L.ST(k, IpmLayout::RD + i)] = d[i];
+            for (int j = 0; j < 6; ++j) snext[j] = cw[j];
             unext[0] = u[0]; unext[1] = u[1];
-            if (k >= 1) { up[0] = um[0]; up[1] = um[1]; }
         }
         return true;
     }
 
     // -------------------------------------------------------- forward pass
-    // Step (dw) and new multipliers (YP) from the Riccati records; also the
+    // Step (DW) and new multipliers (YP) from the Riccati records; also the
     // fraction-to-the-boundary step sizes, grad(phi)^T dw and the tiny-step measure.
     struct Fwd {
         T amax_p, amax_z, gd, rel;
     };
 
-    MPCG_HD void dir_var(int i, T w, T lo, T hi, T gphi, T dwv, Fwd& F) const {
-        const T zl = ws[L.ZL(i)], zu = ws[L.ZU(i)];
+    // branchless: every candidate ratio is computed with one reciprocal and selected
+    MPCG_HD void dir_var(T w, T zl, T zu, T lo, T hi, T gphi, T dwv, Fwd& F) const {
         const T dl = w - lo, du = hi - w;
-        if (dwv < 0) F.amax_p = tmin(F.amax_p, -tau * dl / dwv);
-        if (dwv > 0) F.amax_p = tmin(F.amax_p, tau * du / dwv);
-        const T dzl = mu / dl - zl - zl / dl * dwv;
-        const T dzu = mu / du - zu + zu / du * dwv;
-        if (dzl < 0) F.amax_z = tmin(F.amax_z, -tau * zl / dzl);
-        if (dzu < 0) F.amax_z = tmin(F.amax_z, -tau * zu / dzu);
+        const T rdl = rcp(dl), rdu = rcp(du), rdw = rcp(dwv);
+        const T inf = (T)INFINITY;
+        F.amax_p = tmin(F.amax_p, dwv < 0 ? -tau * dl * rdw : (dwv > 0 ? tau * du * rdw : inf));
+        const T dzl = mu * rdl - zl - zl * rdl * dwv;
+        const T dzu = mu * rdu - zu + zu * rdu * dwv;
+        F.amax_z = tmin(F.amax_z, dzl < 0 ? -tau * zl * rcp(dzl) : inf);
+        F.amax_z = tmin(F.amax_z, dzu < 0 ? -tau * zu * rcp(dzu) : inf);
         F.gd += gphi * dwv;
-        F.rel = tmax(F.rel, (T)fabs(dwv) / ((T)1 + (T)fabs(w)));
+        F.rel = tmax(F.rel, (T)fabs(dwv) * rcp((T)1 + (T)fabs(w)));
     }
 
-    MPCG_HD Fwd forward(int mode) {
+    MPCG_PASS Fwd forward(int mode) {
         Fwd F{(T)1, (T)1, (T)0, (T)0};
         T ds[8];
-        {
-            T s0[6];
-            load_s(0, s0);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) ds[j] = (mode == 0) ? -(s0[j] - pr.init[j]) : (T)0;
-            ds[6] = 0; ds[7] = 0;
+        T cw[8], czl[8], czu[8], nw_[8], nzl[8], nzu[8];
+        ld8(L.W(0, 0), cw);
+        if (mode == 0) {
+            ld8(L.ZL(0, 0), czl);
+            ld8(L.ZU(0, 0), czu);
         }
-        T um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
-        if (N >= 2) load_u(0, u);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) ds[j] = (mode == 0) ? -(cw[j] - pr.init[j]) : (T)0;
+        ds[6] = 0; ds[7] = 0;
+        T um[2] = {0, 0};
         for (int k = 0; k < N; ++k) {
+            const bool last = (k == N - 1);
             T Pm[36], pv[8];
 #pragma unroll
-            for (int i = 0; i < 36; ++i) Pm[i] = ws[L.ST(k, IpmLayout::RP + i)];
+            for (int i = 0; i < 36; i += 2) ws.ld2(L.REC(k, IpmLayout::RP + i), Pm[i], Pm[i + 1]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) pv[i] = ws[L.ST(k, IpmLayout::Rp + i)];
+            for (int i = 0; i < 8; i += 2) ws.ld2(L.REC(k, IpmLayout::Rp + i), pv[i], pv[i + 1]);
+            T K[16], kf[2], a[8], d[6];
+            if (!last) {
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) ws.ld2(L.REC(k, IpmLayout::RK + i), K[i], K[i + 1]);
+                ws.ld2(L.REC(k, IpmLayout::RKFF), kf[0], kf[1]);
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) ws.ld2(L.REC(k, IpmLayout::RA + i), a[i], a[i + 1]);
+#pragma unroll
+                for (int i = 0; i < 6; i += 2) ws.ld2(L.REC(k, IpmLayout::RD + i), d[i], d[i + 1]);
+                ld8(L.W(k + 1, 0), nw_);  // prefetch next stage
+                if (mode == 0) {
+                    ld8(L.ZL(k + 1, 0), nzl);
+                    ld8(L.ZU(k + 1, 0), nzu);
+                }
+            }
             // multipliers of rows (., k): yh+ = -(P ds + p)[0:6]
+            T yp[6];
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 T acc = pv[j];
 #pragma unroll
                 for (int m = 0; m < 8; ++m) acc += Pm[pidx(j, m)] * ds[m];
-                ws[L.YP(L.row(j, k))] = -acc;
+                yp[j] = -acc;
             }
-            T s[6];
-            load_s(k, s);
-            T g[6];
-            grad_state(s, g);
+            st6(L.YP(k, 0), yp);
+            T dk[8];
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const int i = L.vs(j, k);
-                ws[L.DW(i)] = ds[j];
-                if (mode == 0) {
-                    const T gphi = sf * g[j] - mu / (s[j] - sl) + mu / (su - s[j]);
-                    dir_var(i, s[j], sl, su, gphi, ds[j], F);
+            for (int j = 0; j < 6; ++j) dk[j] = ds[j];
+            dk[6] = 0; dk[7] = 0;
+            if (!last) {
+                T du0 = kf[0], du1 = kf[1];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    du0 += K[m] * ds[m];
+                    du1 += K[8 + m] * ds[m];
+                }
+                dk[6] = du0; dk[7] = du1;
+            }
+            st8(L.DW(k, 0), dk);
+            if (mode == 0) {
+                T g[6];
+                grad_state(cw, g);
+                T gu[2] = {0, 0};
+                if (!last) {
+                    const T up[2] = {nw_[6], nw_[7]};
+                    grad_ctrl(k, um, cw + 6, up, gu);
+                }
+                const int nv = last ? 6 : 8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (j < nv) {
+                        const T gj = j < 6 ? sf * g[j] : sf * gu[j - 6];
+                        const T gphi = gj - mu * rcp(cw[j] - vlo(j)) + mu * rcp(vhi(j) - cw[j]);
+                        dir_var(cw[j], czl[j], czu[j], vlo(j), vhi(j), gphi, dk[j], F);
+                    }
                 }
             }
-            if (k == N - 1) break;
-            if (k + 1 < N - 1) load_u(k + 1, up);
-            T K[16], kf[2], a[7], d[6];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) K[i] = ws[L.ST(k, IpmLayout::RK + i)];
-            kf[0] = ws[L.ST(k, IpmLayout::RKFF)];
-            kf[1] = ws[L.ST(k, IpmLayout::RKFF + 1)];
-#pragma unroll
-            for (int i = 0; i < 7; ++i) a[i] = ws[L.ST(k, IpmLayout::RA + i)];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) d[i] = ws[L.ST(k, IpmLayout::RD + i)];
-            T du0 = kf[0], du1 = kf[1];
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                du0 += K[m] * ds[m];
-                du1 += K[8 + m] * ds[m];
-            }
-            const T duv[2] = {du0, du1};
-            T gu[2];
-            grad_ctrl(k, um, u, up, gu);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int i = L.vu(j, k);
-                ws[L.DW(i)] = duv[j];
-                if (mode == 0) {
-                    const T gphi = sf * gu[j] - mu / (u[j] - clo(j)) + mu / (chi(j) - u[j]);
-                    dir_var(i, u[j], clo(j), chi(j), gphi, duv[j], F);
-                }
-            }
+            if (last) break;
             T nx6[6];
             A_mul(a, ds, nx6);
-            nx6[2] += dt * du0;
-            nx6[3] += dt * du1;
-            nx6[5] += dt * du0;
+            nx6[2] += dt * dk[6];
+            nx6[3] += dt * dk[7];
+            nx6[5] += dt * dk[6];
 #pragma unroll
             for (int j = 0; j < 6; ++j) ds[j] = nx6[j] + d[j];
-            ds[6] = du0;
-            ds[7] = du1;
-            um[0] = u[0]; um[1] = u[1];
-            u[0] = up[0]; u[1] = up[1];
+            ds[6] = dk[6];
+            ds[7] = dk[7];
+            um[0] = cw[6]; um[1] = cw[7];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { cw[j] = nw_[j]; czl[j] = nzl[j]; czu[j] = nzu[j]; }
         }
         return F;
     }
 
     // ------------------------------------------------------------ trial point
     // phi_mu and theta at w + alpha dw; returns false if outside the relaxed box.
-    MPCG_HD bool trial(T alpha, T* phi, T* th) const {
+    MPCG_PASS bool trial(T alpha, T* phi, T* th) const {
         LogAcc<T> la;
         la.init();
         T f = 0, thv = 0;
-        T Fprev[6], um[2] = {0, 0}, u[2] = {0, 0}, up[2] = {0, 0};
+        T Fprev[6] = {0, 0, 0, 0, 0, 0};
         bool ok = true;
-        auto tv = [&](int i) -> T { return ws[L.W(i)] + alpha * ws[L.DW(i)]; };
-        if (N >= 2) { u[0] = tv(L.vu(0, 0)); u[1] = tv(L.vu(1, 0)); }
+        T cw[8], cd[8], nw_[8], nd[8];
+        ld8(L.W(0, 0), cw);
+        ld8(L.DW(0, 0), cd);
         for (int k = 0; k < N; ++k) {
-            T s[6];
+            const bool last = (k == N - 1);
+            if (!last) {
+                ld8(L.W(k + 1, 0), nw_);
+                ld8(L.DW(k + 1, 0), nd);
+            }
+            T w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = cw[j] + alpha * cd[j];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    ok = ok && (dl > 0) && (du > 0);
+                    slackprod *= dl * du;
+                }
+            }
+            la.mul(slackprod);
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                s[j] = tv(L.vs(j, k));
-                const T dl = s[j] - sl, du = su - s[j];
-                ok = ok && (dl > 0) && (du > 0);
-                la.mul(dl);
-                la.mul(du);
-                const T c = k == 0 ? s[j] - pr.init[j] : s[j] - Fprev[j];
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
                 thv += fabs(rowscale(j, k) * c);
             }
-            f += cost_state(s);
-            if (k == N - 1) break;
-            if (k + 1 < N - 1) { up[0] = tv(L.vu(0, k + 1)); up[1] = tv(L.vu(1, k + 1)); }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const T dl = u[j] - clo(j), du = chi(j) - u[j];
-                ok = ok && (dl > 0) && (du > 0);
-                la.mul(dl);
-                la.mul(du);
-            }
-            f += (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
-            if (k <= N - 3)
-                f += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
+            f += cost_state(w);
+            if (last) break;
+            T up[2];
+            up[0] = nw_[6] + alpha * nd[6];
+            up[1] = nw_[7] + alpha * nd[7];
+            f += cost_ctrl(k, w + 6, up);
             Lin<T> ln;
-            ln.eval(pr.c, s);
-            ln.next(s, u, dt, Fprev);
-            um[0] = u[0]; um[1] = u[1];
-            u[0] = up[0]; u[1] = up[1];
+            ln.eval(pr.c, w);
+            ln.next(w, w + 6, dt, Fprev);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { cw[j] = nw_[j]; cd[j] = nd[j]; }
         }
         *phi = sf * f - mu * la.value();
         *th = thv;
         return ok && isfinite((double)*phi);
-    }
-
-    // one primal variable and its bound multipliers: z step at the old point, then
-    // z safeguard at the new point (kappa_sigma 1e10)
-    MPCG_HD void accept_var(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun) const {
-        const T ksig = (T)1e10;
-        const T dl = w - lo, du = hi - w;
-        const T dzl = mu / dl - zl - zl / dl * dwv;
-        const T dzu = mu / du - zu + zu / du * dwv;
-        *wn = w + alpha * dwv;
-        const T sl2 = *wn - lo, su2 = hi - *wn;
-        T a = zl + amax_z * dzl, b = zu + amax_z * dzu;
-        *zln = tmax(tmin(a, ksig * mu / sl2), mu / (ksig * sl2));
-        *zun = tmax(tmin(b, ksig * mu / su2), mu / (ksig * su2));
-    }
-
-    // Stage by stage: all loads of a stage first, then the arithmetic, then the stores.
-    MPCG_HD void accept(T alpha, T amax_z) {
-        for (int k = 0; k < N; ++k) {
-            T w[8], dw[8], zl[8], zu[8], y[6], yp[6];
-            const int nv = (k < N - 1) ? 8 : 6;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (j < nv) {
-                    const int i = j < 6 ? L.vs(j, k) : L.vu(j - 6, k);
-                    w[j] = ws[L.W(i)];
-                    dw[j] = ws[L.DW(i)];
-                    zl[j] = ws[L.ZL(i)];
-                    zu[j] = ws[L.ZU(i)];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                y[j] = ws[L.Y(L.row(j, k))];
-                yp[j] = ws[L.YP(L.row(j, k))];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (j < nv) {
-                    const T lo = j < 6 ? sl : (j == 6 ? wl : al);
-                    const T hi = j < 6 ? su : (j == 6 ? wu : au);
-                    T wn, zln, zun;
-                    accept_var(w[j], dw[j], zl[j], zu[j], lo, hi, alpha, amax_z, &wn, &zln, &zun);
-                    const int i = j < 6 ? L.vs(j, k) : L.vu(j - 6, k);
-                    ws[L.W(i)] = wn;
-                    ws[L.ZL(i)] = zln;
-                    ws[L.ZU(i)] = zun;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 6; ++j) ws[L.Y(L.row(j, k))] = y[j] + alpha * (yp[j] - y[j]);
-        }
     }
 
     // ------------------------------------------------------------------ solve
@@ -831,16 +892,25 @@ struct IpmSolver {
         init_point();
         // least-squares multipliers (constr_mult_init_max 1000)
         {
-            bool ok = riccati(1, (T)0);
+            const bool ok = riccati(1, (T)0);
             T ymax = 0;
             if (ok) {
                 forward(1);
-                for (int k = 0; k < N; ++k)
+                for (int k = 0; k < N; ++k) {
+                    T yp[6];
+                    ld6(L.YP(k, 0), yp);
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) ymax = tmax(ymax, (T)fabs(ws[L.YP(L.row(j, k))] / rowscale(j, k)));
+                    for (int j = 0; j < 6; ++j) ymax = tmax(ymax, (T)fabs(yp[j] / rowscale(j, k)));
+                }
             }
             const bool use = ok && ymax <= (T)1000;
-            for (int r = 0; r < L.ng(); ++r) ws[L.Y(r)] = use ? ws[L.YP(r)] : (T)0;
+            for (int k = 0; k < N; ++k) {
+                T yp[6];
+                ld6(L.YP(k, 0), yp);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) yp[j] = use ? yp[j] : (T)0;
+                st6(L.Y(k, 0), yp);
+            }
         }
         mu = (T)P.mu_init;
         const T mu_min = (T)(P.tol / 10.0);
@@ -848,7 +918,7 @@ struct IpmSolver {
         const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
         const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
         const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
-        stats();
+        stats(false, (T)0, (T)0);
         const T theta0 = theta;
         const T theta_max = (T)1e4 * tmax((T)1, theta0);
         const T theta_min = (T)1e-4 * tmax((T)1, theta0);
@@ -857,10 +927,13 @@ struct IpmSolver {
         const int cap = P.filter_cap;
         IpmResult res{IPM_MAXITER, 0, 0.0, 0.0};
         int iter = 0;
-        const int nbnd = 2 * L.nx();
-        const int ng = L.ng();
+        const int nbnd = 2 * (8 * N - 2);
+        const int ng = 6 * N;
+        T acc_alpha = 0, acc_amax_z = 0;
+        MPCG_STAMP_BEGIN();
         for (iter = 0; iter <= P.max_iter; ++iter) {
-            if (iter > 0) stats();
+            if (iter > 0) stats(true, acc_alpha, acc_amax_z);
+            MPCG_STAMP(0);
             const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
             const T sc = tmax((T)100, l1z / (T)nbnd) / (T)100;
             const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / sc));
@@ -900,8 +973,10 @@ struct IpmSolver {
                 ++attempt;
                 if (delta_w > (T)1e40) break;
             }
+            MPCG_STAMP(1);
             if (!ok) { res.status = IPM_ERROR_IN_STEP; break; }
             const Fwd Fd = forward(0);
+            MPCG_STAMP(2);
             // filter line search
             const T phik = sf * fval - mu * logsum;
             const T thetak = theta;
@@ -926,7 +1001,7 @@ struct IpmSolver {
                 if (okt && thetat < theta_max) {
                     bool infilt = false;
                     for (int f = 0; f < nfilter; ++f) {
-                        const T fth = ws[L.FI(2 * f)], fph = ws[L.FI(2 * f + 1)];
+                        const T fth = ws.ld(L.FI(2 * f)), fph = ws.ld(L.FI(2 * f + 1));
                         if (thetat >= fth && phit >= fph) { infilt = true; break; }
                     }
                     if (!infilt) {
@@ -943,31 +1018,33 @@ struct IpmSolver {
                 }
                 alpha *= (T)0.5;
             }
+            MPCG_STAMP(3);
             if (!accepted) { res.status = IPM_RESTORATION_FAILURE; break; }
             if (!ftype) {
                 int slot = nfilter;
                 if (nfilter == cap) {  // full: drop the oldest entry
                     for (int f = 1; f < cap; ++f) {
-                        ws[L.FI(2 * (f - 1))] = ws[L.FI(2 * f)];
-                        ws[L.FI(2 * (f - 1) + 1)] = ws[L.FI(2 * f + 1)];
+                        ws.st(L.FI(2 * (f - 1)), ws.ld(L.FI(2 * f)));
+                        ws.st(L.FI(2 * (f - 1) + 1), ws.ld(L.FI(2 * f + 1)));
                     }
                     slot = cap - 1;
                 } else {
                     ++nfilter;
                 }
-                ws[L.FI(2 * slot)] = ((T)1 - gamma_theta) * thetak;
-                ws[L.FI(2 * slot + 1)] = phik - gamma_phi * thetak;
+                ws.st(L.FI(2 * slot), ((T)1 - gamma_theta) * thetak);
+                ws.st(L.FI(2 * slot + 1), phik - gamma_phi * thetak);
             }
-            accept(alpha, Fd.amax_z);
+            acc_alpha = alpha;         // applied by the next stats() sweep
+            acc_amax_z = Fd.amax_z;
         }
         res.iters = iter;
         return res;
     }
 
     // Final point with honor_original_bounds projection; objective at that point.
-    MPCG_HD T x_state(int j, int k) const { return tmin(tmax((T)ws[L.W(L.vs(j, k))], sl0), su0); }
+    MPCG_HD T x_state(int j, int k) const { return tmin(tmax((T)ws.ld(L.W(k, j)), sl0), su0); }
     MPCG_HD T x_ctrl(int j, int k) const {
-        const T v = ws[L.W(L.vu(j, k))];
+        const T v = ws.ld(L.W(k, 6 + j));
         return j == 0 ? tmin(tmax(v, wl0), wu0) : tmin(tmax(v, al0), au0);
     }
     MPCG_HD T objective_out() const {
@@ -979,12 +1056,10 @@ struct IpmSolver {
             f += cost_state(s);
         }
         for (int k = 0; k < N - 1; ++k) {
-            const T w = x_ctrl(0, k), a = x_ctrl(1, k);
-            f += (T)P.w_w * w * w + (T)P.w_a * a * a;
-            if (k <= N - 3) {
-                const T w1 = x_ctrl(0, k + 1), a1 = x_ctrl(1, k + 1);
-                f += (T)P.w_dw * (w1 - w) * (w1 - w) + (T)P.w_da * (a1 - a) * (a1 - a);
-            }
+            const T u[2] = {x_ctrl(0, k), x_ctrl(1, k)};
+            T up[2] = {0, 0};
+            if (k <= N - 3) { up[0] = x_ctrl(0, k + 1); up[1] = x_ctrl(1, k + 1); }
+            f += cost_ctrl(k, u, up);
         }
         return f;
     }

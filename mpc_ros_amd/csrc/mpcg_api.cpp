@@ -164,7 +164,8 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B) {
     if (!p || B <= 0) return 0;
     const mpcg::IpmLayout L{p->steps};
-    return (size_t)L.total(p->filter_cap) * sizeof(double) * (size_t)B;
+    const size_t tiles = (size_t)((B + 63) / 64);  // one tile of 64 problems per wavefront
+    return (size_t)L.total(p->filter_cap) * sizeof(double) * 64 * tiles;
 }
 
 int mpcg_create(int device, mpcg_handle** out) {

@@ -15,15 +15,34 @@
 
 namespace mpcg {
 
-// Workspace accessor.  The pointer is typed in the global address space so that
-// every access is a global_load/global_store (vmcnt-ordered, pipelinable), never a
-// flat access (which orders against LDS too and forces full drains).
+// Workspace accessor.  The workspace is cut into one tile per wavefront (64
+// problems); element e of lane l in a tile lives at
+//     tile[2 * ((e >> 1) * 64 + l) + (e & 1)]
+// i.e. element pairs (2j, 2j+1) of a problem are adjacent and the pairs of the 64
+// lanes follow each other: a wavefront's pair access is one 1 KB contiguous
+// global_load/store_dwordx4, and every address is a wave-uniform (scalar) base plus
+// one per-lane register.  The pointer is typed in the global address space so that
+// no access is ever a flat access.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MPCG_GLOBAL __attribute__((address_space(1)))
+#else
+#define MPCG_GLOBAL
+#endif
 template <typename T>
 struct DevWs {
-    typedef __attribute__((address_space(1))) T gT;
-    gT* base;
-    int64_t stride;
-    __device__ __forceinline__ gT& operator[](int e) const { return base[(int64_t)e * stride]; }
+    typedef MPCG_GLOBAL T gT;
+    typedef MPCG_GLOBAL double2 gT2;
+    gT* tile;  // wave-uniform: this wavefront's tile
+    int lane;  // 0..63
+    __device__ __forceinline__ gT* at(int e) const { return tile + (((e >> 1) * 64 + lane) << 1) + (e & 1); }
+    __device__ __forceinline__ T ld(int e) const { return *at(e); }
+    __device__ __forceinline__ void st(int e, T v) const { *at(e) = v; }
+    __device__ __forceinline__ void ld2(int e, T& a, T& b) const {
+        const double2 v = *(const gT2*)at(e);
+        a = v.x;
+        b = v.y;
+    }
+    __device__ __forceinline__ void st2(int e, T a, T b) const { *(gT2*)at(e) = make_double2(a, b); }
 };
 
 __global__ void __launch_bounds__(64, 1)
@@ -37,7 +56,9 @@ ipm_solve_kernel(IpmParams P, int64_t B, const double* __restrict__ state, const
     for (int j = 0; j < 6; ++j) pr.init[j] = state[p * 6 + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) pr.c[j] = coeffs[p * 4 + j];
-    DevWs<double> w{(DevWs<double>::gT*)(ws + p), B};
+    const IpmLayout Lw{P.N};
+    const int64_t tile_elems = (int64_t)Lw.total(P.filter_cap) * 64;
+    DevWs<double> w{(DevWs<double>::gT*)(ws + (int64_t)blockIdx.x * tile_elems), (int)threadIdx.x};
     IpmSolver<double, DevWs<double>> S(P, pr, w);
     const IpmResult r = S.solve();
     u0[p * 2 + 0] = S.x_ctrl(0, 0);

@@ -14,9 +14,13 @@
 
 #include "../../mpc_ros_amd/csrc/ipm_core.h"
 
+// single-problem workspace: the pair-interleaved layout degenerates to identity
 struct HostWs {
     double* base;
-    double& operator[](int e) const { return base[e]; }
+    double ld(int e) const { return base[e]; }
+    void st(int e, double v) const { base[e] = v; }
+    void ld2(int e, double& a, double& b) const { a = base[e]; b = base[e + 1]; }
+    void st2(int e, double a, double b) const { base[e] = a; base[e + 1] = b; }
 };
 
 int main() {
@@ -31,6 +35,7 @@ int main() {
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     mpcg::IpmLayout L{P.N};
+    (void)L;
     std::vector<double> buf(L.total(P.filter_cap));
     for (long b = 0; b < B; ++b) {
         mpcg::IpmProblem<double> pr;

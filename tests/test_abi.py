@@ -79,8 +79,10 @@ def test_workspace_bytes(libmpcg):
 
     p = _lib.MpcgParams()
     libmpcg.mpcg_params_plugin_default(C.byref(p))
-    b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
-    assert b1 > 0 and libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) == 65536 * b1
+    b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)  # one 64-problem wavefront tile
+    assert b1 > 0 and libmpcg.mpcg_workspace_bytes(C.byref(p), 64) == b1
+    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65) == 2 * b1
+    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) == 1024 * b1
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
 
 
