@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--gather-traj", action="store_true", help="also gather the 3N trajectories")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--profile-name", default=None, help="PMC summary to read traffic from")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "lane", "wave"],
+                    help="kernel strategy: one problem per lane / per wavefront")
     return ap.parse_args()
 
 
@@ -105,7 +107,7 @@ def main():
     st, cf = infinity.make_problems(np.arange(start, start + count))
     tst = torch.from_numpy(st).to(dev)
     tcf = torch.from_numpy(cf).to(dev)
-    solver = BatchSolver(dev.index, P)
+    solver = BatchSolver(dev.index, P, strategy=a.strategy)
     solver.reserve(count)
     u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
     traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)

@@ -99,9 +99,13 @@ int mpcg_reserve(mpcg_handle* h, int64_t B);
 int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0,
                double* traj, int32_t* status, double* obj, int32_t* iters);
 
-/* Batched solve on device-resident buffers (same layouts), asynchronous on `stream`
- * (a hipStream_t; NULL = the null stream, as everywhere in HIP).  No host synchronisation, no
- * allocation if mpcg_reserve(h, B) was called: safe to capture in a HIP graph. */
+/* Batched solve on device-resident buffers (same layouts), queued on `stream` (a
+ * hipStream_t; NULL = the null stream, as everywhere in HIP).  The interior-point
+ * iterations are launched in chunks; the call returns once a device-side counter
+ * shows every problem terminated (one small event wait per chunk, overlapped with the
+ * next chunk).  The outputs are written by the last kernel queued on `stream`:
+ * synchronise the stream before reading them on the host.  No allocation if
+ * mpcg_reserve(h, B) was called. */
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
 
@@ -112,6 +116,18 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
 int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
                            const double* d_plan, int32_t delay_mode, double* d_state, double* d_coeffs,
                            void* stream);
+
+/* Kernel strategy of the handle's solves (performance only: every strategy runs the
+ * same algorithm, results agree to rounding):
+ *   MPCG_STRATEGY_AUTO  one problem per wavefront when it fits (steps <= 64), else per lane
+ *   MPCG_STRATEGY_LANE  one problem per lane, 64 problems per wavefront, state in HBM
+ *   MPCG_STRATEGY_WAVE  one problem per wavefront, the whole problem state in LDS */
+#define MPCG_STRATEGY_AUTO 0
+#define MPCG_STRATEGY_LANE 1
+#define MPCG_STRATEGY_WAVE 2
+int mpcg_set_strategy(mpcg_handle* h, int32_t strategy);
+/* The strategy a solve of the handle's current parameters would use (never AUTO). */
+int mpcg_get_strategy(const mpcg_handle* h);
 
 /* Wait for all work queued on the handle's stream. */
 int mpcg_synchronize(mpcg_handle* h);

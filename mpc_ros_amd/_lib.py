@@ -54,7 +54,11 @@ SIGNATURES = {
     "mpcg_preprocess_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                 C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_synchronize": ([C.c_void_p], C.c_int),
+    "mpcg_set_strategy": ([C.c_void_p, C.c_int32], C.c_int),
+    "mpcg_get_strategy": ([C.c_void_p], C.c_int),
 }
+
+STRATEGY = {"auto": 0, "lane": 1, "wave": 2}
 
 _lib = None
 

@@ -87,7 +87,23 @@ struct IpmLayout {
     MPCG_HD int YP(int k, int j) const { return 40 * N + 8 * k + j; }
     MPCG_HD int REC(int k, int j) const { return 48 * N + RS * k + j; }
     MPCG_HD int FI(int j) const { return 128 * N + j; }
-    MPCG_HD int total(int cap) const { return 128 * N + 2 * cap + 2; }
+    // per-problem scalar state between the phase kernels (SC_* below), after the filter
+    int cap;
+    MPCG_HD int SC(int j) const { return 128 * N + 2 * cap + 2 + j; }
+    MPCG_HD int total(int cap_) const { return 128 * N + 2 * cap_ + 2 + 32; }
+};
+
+// Scalar state of one problem, stored in its workspace between phase kernels.
+enum : int {
+    SC_SF = 0,          // objective scale
+    SC_RA = 1,          // 6 row scales of the dynamics rows into stage 1
+    SC_RB = 7,          // 6 row scales of the dynamics rows into stages >= 2
+    SC_MU = 13, SC_TAU = 14, SC_THMAX = 15, SC_THMIN = 16, SC_DWLAST = 17,
+    SC_ACCA = 18, SC_ACCZ = 19,                       // accepted step, applied by the next stats sweep
+    SC_AMAXP = 20, SC_AMAXZ = 21, SC_GD = 22, SC_REL = 23,  // direction statistics
+    SC_FVAL = 24, SC_LOGSUM = 25, SC_THETA = 26,      // objective, barrier log-sum, violation at the iterate
+    SC_ITER = 27, SC_NFILTER = 28, SC_STATUS = 29,    // status 0 = still iterating
+    SC_KKT = 30, SC_LSOK = 31,
 };
 
 template <typename T>
@@ -103,14 +119,58 @@ struct IpmResult {
     double kkt_inf;
 };
 
-template <typename T>
-MPCG_HD void sc_t(T a, T* s, T* c) {
+// sin and cos of one angle.  |a| < 2^19 pi/2 (every angle a bounded trajectory can
+// reach): Cody-Waite reduction by pi/2 with a three-part constant and FMA, then the
+// fdlibm minimax kernels on [-pi/4, pi/4] (degree 13 / 14) and quadrant selection --
+// ~35 instructions, within 1-2 ulp of the correctly rounded values.  Larger
+// arguments take the library routine.
+MPCG_HD void sincos_small(double a, double* s, double* c) {
+    const double inv_pio2 = 6.36619772367581382433e-01;
+    const double p1 = 1.57079632679489655800e+00, p2 = 6.12323399573676603587e-17, p3 = -1.49738490485916983e-33;
+    const double n = rint(a * inv_pio2);
+    double r = __builtin_fma(-n, p1, a);
+    r = __builtin_fma(-n, p2, r);
+    r = __builtin_fma(-n, p3, r);
+    const double z = r * r;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double ps = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double sr = __builtin_fma(r * z, __builtin_fma(z, ps, S1), r);
+    const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * pc);
+    const int q = (int)((long long)n & 3);
+    const double sv = (q & 1) ? cr : sr;
+    const double cv = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -sv : sv;
+    *c = ((q + 1) & 2) ? -cv : cv;
+}
+
+#if defined(__HIPCC__)
+static __host__ __device__ __attribute__((noinline))
+#else
+static inline
+#endif
+void sincos_large(double a, double* s, double* c) {
 #if defined(__HIP_DEVICE_COMPILE__)
     sincos(a, s, c);
 #else
     *s = sin(a);
     *c = cos(a);
 #endif
+}
+
+template <typename T>
+MPCG_HD void sc_t(T a, T* s, T* c) {
+    if (__builtin_expect(fabs(a) < 823549.6, 1))
+        sincos_small(a, s, c);
+    else
+        sincos_large(a, s, c);  // out of line: never reached by a bounded trajectory
 }
 
 template <typename T>
@@ -206,21 +266,6 @@ MPCG_HD void A_mul(const T* a, const T* x, T* y) {
 MPCG_HD constexpr int pidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
 
-// Diagnostic cycle stamps (tools/diag_stamps.hip only; never in the product build).
-#if defined(MPCG_DIAG)
-#define MPCG_STAMP_DECL uint64_t tacc[6] = {0, 0, 0, 0, 0, 0}; uint64_t tlast = 0;
-#endif
-#if defined(MPCG_DIAG) && defined(__HIP_DEVICE_COMPILE__)
-#define MPCG_STAMP_BEGIN() (tlast = __builtin_amdgcn_s_memtime())
-#define MPCG_STAMP(slot) do { uint64_t _t = __builtin_amdgcn_s_memtime(); tacc[slot] += _t - tlast; tlast = _t; } while (0)
-#else
-#if !defined(MPCG_DIAG)
-#define MPCG_STAMP_DECL
-#endif
-#define MPCG_STAMP_BEGIN() ((void)0)
-#define MPCG_STAMP(slot) ((void)0)
-#endif
-
 // One stage's iterate as loaded from the workspace.
 template <typename T>
 struct StageIt {
@@ -229,7 +274,6 @@ struct StageIt {
 
 template <typename T, class WS>
 struct IpmSolver {
-    MPCG_STAMP_DECL
     // held by value: a reference member would force the kernel-argument structs into
     // private (scratch) memory and turn every workspace access into a flat access
     const IpmParams P;
@@ -251,7 +295,7 @@ struct IpmSolver {
     int nfilter;
 
     MPCG_HD IpmSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WS& ws_)
-        : P(P_), pr(pr_), ws(ws_), L{P_.N}, N(P_.N), dt((T)P_.dt) {}
+        : P(P_), pr(pr_), ws(ws_), L{P_.N, P_.filter_cap}, N(P_.N), dt((T)P_.dt) {}
 
     // -------------------------------------------------------- memory helpers
     MPCG_HD void ld8(int e, T* v) const {
@@ -886,159 +930,291 @@ struct IpmSolver {
         return ok && isfinite((double)*phi);
     }
 
-    // ------------------------------------------------------------------ solve
-    MPCG_HD IpmResult solve() {
+    // ------------------------------------------------------------ phases
+    // The IPM is run as a sequence of phases, each a separate kernel on the device
+    // (mpcg_kernels.hip) so that each gets its own register allocation; between
+    // phases a problem's scalar state lives in its workspace (SC_*).
+    //   init0 -> newton(1) -> direction(1) -> init1 -> { begin -> newton(0) ->
+    //   direction(0) -> linesearch }* -> outputs
+    // The same sequence run in a loop on one problem is exactly solve() below.
+    MPCG_HD T sc(int j) const { return ws.ld(L.SC(j)); }
+    MPCG_HD void set_sc(int j, T v) const { ws.st(L.SC(j), v); }
+    MPCG_HD int status() const { return (int)sc(SC_STATUS); }
+    MPCG_HD void load_scales() {
+        sf = sc(SC_SF);
+        ra0 = sc(SC_RA + 0); ra1 = sc(SC_RA + 1); ra2 = sc(SC_RA + 2);
+        ra3 = sc(SC_RA + 3); ra4 = sc(SC_RA + 4); ra5 = sc(SC_RA + 5);
+        rb0 = sc(SC_RB + 0); rb1 = sc(SC_RB + 1); rb2 = sc(SC_RB + 2);
+        rb3 = sc(SC_RB + 3); rb4 = sc(SC_RB + 4); rb5 = sc(SC_RB + 5);
+    }
+    MPCG_HD void bounds_only() {
+        const T rl = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.bound));
+        sl0 = (T)-P.bound; su0 = (T)P.bound; sl = sl0 - rl; su = su0 + rl;
+        const T rw = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_w));
+        wl0 = (T)-P.max_w; wu0 = (T)P.max_w; wl = wl0 - rw; wu = wu0 + rw;
+        const T ra = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_a));
+        al0 = (T)-P.max_a; au0 = (T)P.max_a; al = al0 - ra; au = au0 + ra;
+    }
+    // common prologue of every phase after init0
+    MPCG_HD void restore() {
+        bounds_only();
+        load_scales();
+        mu = sc(SC_MU);
+        tau = sc(SC_TAU);
+    }
+
+    // init0: bounds, scaling, starting point, bound multipliers.
+    MPCG_HD void phase_init0() {
         setup();
         init_point();
-        // least-squares multipliers (constr_mult_init_max 1000)
-        {
-            const bool ok = riccati(1, (T)0);
-            T ymax = 0;
-            if (ok) {
-                forward(1);
-                for (int k = 0; k < N; ++k) {
-                    T yp[6];
-                    ld6(L.YP(k, 0), yp);
-#pragma unroll
-                    for (int j = 0; j < 6; ++j) ymax = tmax(ymax, (T)fabs(yp[j] / rowscale(j, k)));
-                }
-            }
-            const bool use = ok && ymax <= (T)1000;
+        set_sc(SC_SF, sf);
+        set_sc(SC_RA + 0, ra0); set_sc(SC_RA + 1, ra1); set_sc(SC_RA + 2, ra2);
+        set_sc(SC_RA + 3, ra3); set_sc(SC_RA + 4, ra4); set_sc(SC_RA + 5, ra5);
+        set_sc(SC_RB + 0, rb0); set_sc(SC_RB + 1, rb1); set_sc(SC_RB + 2, rb2);
+        set_sc(SC_RB + 3, rb3); set_sc(SC_RB + 4, rb4); set_sc(SC_RB + 5, rb5);
+        set_sc(SC_MU, (T)P.mu_init);
+        set_sc(SC_TAU, tmax((T)0.99, (T)1 - (T)P.mu_init));
+        set_sc(SC_STATUS, 0);
+    }
+
+    // init1: least-squares multipliers (constr_mult_init_max 1000) from the mode-1
+    // Newton/direction phases, then the statistics of the starting point.
+    MPCG_HD void phase_init1() {
+        restore();
+        const bool ok = sc(SC_LSOK) != 0;
+        T ymax = 0;
+        if (ok) {
             for (int k = 0; k < N; ++k) {
                 T yp[6];
                 ld6(L.YP(k, 0), yp);
 #pragma unroll
-                for (int j = 0; j < 6; ++j) yp[j] = use ? yp[j] : (T)0;
-                st6(L.Y(k, 0), yp);
+                for (int j = 0; j < 6; ++j) ymax = tmax(ymax, (T)fabs(yp[j] * rcp(rowscale(j, k))));
             }
         }
-        mu = (T)P.mu_init;
-        const T mu_min = (T)(P.tol / 10.0);
-        tau = tmax((T)0.99, (T)1 - mu);
-        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
-        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
-        const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
+        const bool use = ok && ymax <= (T)1000;
+        for (int k = 0; k < N; ++k) {
+            T yp[6];
+            ld6(L.YP(k, 0), yp);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) yp[j] = use ? yp[j] : (T)0;
+            st6(L.Y(k, 0), yp);
+        }
         stats(false, (T)0, (T)0);
-        const T theta0 = theta;
-        const T theta_max = (T)1e4 * tmax((T)1, theta0);
-        const T theta_min = (T)1e-4 * tmax((T)1, theta0);
-        T delta_w_last = 0;
-        nfilter = 0;
-        const int cap = P.filter_cap;
-        IpmResult res{IPM_MAXITER, 0, 0.0, 0.0};
-        int iter = 0;
+        set_sc(SC_THMAX, (T)1e4 * tmax((T)1, theta));
+        set_sc(SC_THMIN, (T)1e-4 * tmax((T)1, theta));
+        set_sc(SC_DWLAST, 0);
+        set_sc(SC_ACCA, 0);
+        set_sc(SC_ACCZ, 0);
+        set_sc(SC_ITER, 0);
+        set_sc(SC_NFILTER, 0);
+        set_sc(SC_KKT, 0);
+    }
+
+    // begin: apply the accepted step of the previous iteration, statistics,
+    // termination tests, monotone barrier update.  Returns the new status
+    // (0 = keep iterating).
+    MPCG_HD int phase_begin() {
+        restore();
+        const int iter = (int)sc(SC_ITER);
+        stats(iter > 0, sc(SC_ACCA), sc(SC_ACCZ));
         const int nbnd = 2 * (8 * N - 2);
         const int ng = 6 * N;
-        T acc_alpha = 0, acc_amax_z = 0;
-        MPCG_STAMP_BEGIN();
-        for (iter = 0; iter <= P.max_iter; ++iter) {
-            if (iter > 0) stats(true, acc_alpha, acc_amax_z);
-            MPCG_STAMP(0);
-            const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
-            const T sc = tmax((T)100, l1z / (T)nbnd) / (T)100;
-            const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / sc));
-            const T dual_uns = dual_inf / sf;
-            res.kkt_inf = (double)tmax(dual_uns, tmax(prim_uns, compl0));
-            if (!isfinite((double)E0)) { res.status = IPM_INVALID_NUMBER; break; }
-            if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4) {
-                res.status = IPM_SUCCESS;
+        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
+        const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
+        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
+        const T dual_uns = dual_inf / sf;
+        set_sc(SC_KKT, tmax(dual_uns, tmax(prim_uns, compl0)));
+        int st = 0;
+        if (!isfinite((double)E0))
+            st = IPM_INVALID_NUMBER;
+        else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4)
+            st = IPM_SUCCESS;
+        else if (iter == P.max_iter)
+            st = IPM_MAXITER;
+        if (st) {
+            set_sc(SC_STATUS, st);
+            return st;
+        }
+        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
+        const T mu_min = (T)(P.tol / 10.0);
+        int nf = (int)sc(SC_NFILTER);
+        for (;;) {
+            const T complmu = tmax(pmax - mu, mu - pmin);
+            const T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+            if (Emu > kappa_eps * mu || mu <= mu_min) break;
+            const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
+            if (mnew >= mu) break;
+            mu = mnew;
+            tau = tmax((T)0.99, (T)1 - mu);
+            nf = 0;
+        }
+        set_sc(SC_MU, mu);
+        set_sc(SC_TAU, tau);
+        set_sc(SC_NFILTER, (T)nf);
+        set_sc(SC_FVAL, fval);
+        set_sc(SC_LOGSUM, logsum);
+        set_sc(SC_THETA, theta);
+        return 0;
+    }
+
+    // newton: mode 0 = Newton step of the barrier problem with Ipopt's inertia
+    // correction (delta_w schedule); mode 1 = least-squares multiplier system.
+    MPCG_HD int phase_newton(int mode) {
+        restore();
+        if (mode == 1) {
+            set_sc(SC_LSOK, riccati(1, (T)0) ? (T)1 : (T)0);
+            return 0;
+        }
+        T delta_w_last = sc(SC_DWLAST);
+        T delta_w = 0;
+        int attempt = 0;
+        bool ok = false;
+        for (;;) {
+            if (riccati(0, delta_w)) {
+                ok = true;
+                if (delta_w > 0) delta_w_last = delta_w;
                 break;
             }
-            if (iter == P.max_iter) { res.status = IPM_MAXITER; break; }
-            // monotone barrier update (possibly several times)
-            for (;;) {
-                const T complmu = tmax(pmax - mu, mu - pmin);
-                const T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / sc));
-                if (Emu > kappa_eps * mu || mu <= mu_min) break;
-                const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
-                if (mnew >= mu) break;
-                mu = mnew;
-                tau = tmax((T)0.99, (T)1 - mu);
-                nfilter = 0;
-            }
-            // Newton step with inertia correction
-            T delta_w = 0;
-            int attempt = 0;
-            bool ok = false;
-            for (;;) {
-                if (riccati(0, delta_w)) {
-                    ok = true;
-                    if (delta_w > 0) delta_w_last = delta_w;
-                    break;
-                }
-                if (attempt == 0)
-                    delta_w = (delta_w_last == 0) ? (T)1e-4 : tmax((T)1e-20, delta_w_last / (T)3);
-                else
-                    delta_w = (delta_w_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
-                ++attempt;
-                if (delta_w > (T)1e40) break;
-            }
-            MPCG_STAMP(1);
-            if (!ok) { res.status = IPM_ERROR_IN_STEP; break; }
-            const Fwd Fd = forward(0);
-            MPCG_STAMP(2);
-            // filter line search
-            const T phik = sf * fval - mu * logsum;
-            const T thetak = theta;
-            const T gd = Fd.gd;
-            T alpha_min;
-            if (gd < 0 && thetak <= theta_min)
-                alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd,
-                                                                 delta_sw * (T)pow((double)thetak, (double)s_theta) /
-                                                                     (T)pow((double)-gd, (double)s_phi)));
-            else if (gd < 0)
-                alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
+            if (attempt == 0)
+                delta_w = (delta_w_last == 0) ? (T)1e-4 : tmax((T)1e-20, delta_w_last / (T)3);
             else
-                alpha_min = gamma_alpha * gamma_theta;
-            const bool tiny = Fd.rel < (T)(10.0 * 2.2e-16);
-            T alpha = Fd.amax_p;
-            bool accepted = false, ftype = false;
-            for (int ls = 0; ls < 60; ++ls) {
-                if (tiny) { accepted = true; ftype = true; break; }
-                if (alpha < alpha_min) break;
-                T phit, thetat;
-                const bool okt = trial(alpha, &phit, &thetat);
-                if (okt && thetat < theta_max) {
-                    bool infilt = false;
-                    for (int f = 0; f < nfilter; ++f) {
-                        const T fth = ws.ld(L.FI(2 * f)), fph = ws.ld(L.FI(2 * f + 1));
-                        if (thetat >= fth && phit >= fph) { infilt = true; break; }
-                    }
-                    if (!infilt) {
-                        const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
-                                                     delta_sw * (T)pow((double)thetak, (double)s_theta));
-                        if (thetak <= theta_min && sw) {
-                            if (phit <= phik + eta_phi * alpha * gd) { accepted = true; ftype = true; break; }
-                        } else if (thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak) {
-                            accepted = true;
-                            ftype = false;
-                            break;
-                        }
-                    }
-                }
-                alpha *= (T)0.5;
-            }
-            MPCG_STAMP(3);
-            if (!accepted) { res.status = IPM_RESTORATION_FAILURE; break; }
-            if (!ftype) {
-                int slot = nfilter;
-                if (nfilter == cap) {  // full: drop the oldest entry
-                    for (int f = 1; f < cap; ++f) {
-                        ws.st(L.FI(2 * (f - 1)), ws.ld(L.FI(2 * f)));
-                        ws.st(L.FI(2 * (f - 1) + 1), ws.ld(L.FI(2 * f + 1)));
-                    }
-                    slot = cap - 1;
-                } else {
-                    ++nfilter;
-                }
-                ws.st(L.FI(2 * slot), ((T)1 - gamma_theta) * thetak);
-                ws.st(L.FI(2 * slot + 1), phik - gamma_phi * thetak);
-            }
-            acc_alpha = alpha;         // applied by the next stats() sweep
-            acc_amax_z = Fd.amax_z;
+                delta_w = (delta_w_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
+            ++attempt;
+            if (delta_w > (T)1e40) break;
         }
-        res.iters = iter;
-        return res;
+        set_sc(SC_DWLAST, delta_w_last);
+        if (!ok) {
+            set_sc(SC_STATUS, IPM_ERROR_IN_STEP);
+            return IPM_ERROR_IN_STEP;
+        }
+        return 0;
+    }
+
+    // direction: step, new multipliers, fraction-to-the-boundary statistics.
+    MPCG_HD void phase_direction(int mode) {
+        restore();
+        const Fwd F = forward(mode);
+        if (mode == 0) {
+            set_sc(SC_AMAXP, F.amax_p);
+            set_sc(SC_AMAXZ, F.amax_z);
+            set_sc(SC_GD, F.gd);
+            set_sc(SC_REL, F.rel);
+        }
+    }
+
+    // linesearch: Ipopt's filter line search; records the accepted step for the
+    // next begin phase.  Returns the new status (0 = keep iterating).
+    MPCG_HD int phase_linesearch() {
+        restore();
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
+        const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
+        const T theta_max = sc(SC_THMAX), theta_min = sc(SC_THMIN);
+        const T phik = sf * sc(SC_FVAL) - mu * sc(SC_LOGSUM);
+        const T thetak = sc(SC_THETA);
+        const T gd = sc(SC_GD);
+        int nf = (int)sc(SC_NFILTER);
+        const int cap = P.filter_cap;
+        T alpha_min;
+        if (gd < 0 && thetak <= theta_min)
+            alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd,
+                                                             delta_sw * (T)pow((double)thetak, (double)s_theta) /
+                                                                 (T)pow((double)-gd, (double)s_phi)));
+        else if (gd < 0)
+            alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
+        else
+            alpha_min = gamma_alpha * gamma_theta;
+        const bool tiny = sc(SC_REL) < (T)(10.0 * 2.2e-16);
+        T alpha = sc(SC_AMAXP);
+        bool accepted = false, ftype = false;
+        for (int ls = 0; ls < 60; ++ls) {
+            if (tiny) { accepted = true; ftype = true; break; }
+            if (alpha < alpha_min) break;
+            T phit, thetat;
+            const bool okt = trial(alpha, &phit, &thetat);
+            if (okt && thetat < theta_max) {
+                bool infilt = false;
+                for (int f = 0; f < nf; ++f) {
+                    const T fth = ws.ld(L.FI(2 * f)), fph = ws.ld(L.FI(2 * f + 1));
+                    if (thetat >= fth && phit >= fph) { infilt = true; break; }
+                }
+                if (!infilt) {
+                    const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
+                                                 delta_sw * (T)pow((double)thetak, (double)s_theta));
+                    if (thetak <= theta_min && sw) {
+                        if (phit <= phik + eta_phi * alpha * gd) { accepted = true; ftype = true; break; }
+                    } else if (thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak) {
+                        accepted = true;
+                        ftype = false;
+                        break;
+                    }
+                }
+            }
+            alpha *= (T)0.5;
+        }
+        if (!accepted) {
+            set_sc(SC_STATUS, IPM_RESTORATION_FAILURE);
+            return IPM_RESTORATION_FAILURE;
+        }
+        if (!ftype) {
+            int slot = nf;
+            if (nf == cap) {  // full: drop the oldest entry
+                for (int f = 1; f < cap; ++f) {
+                    ws.st(L.FI(2 * (f - 1)), ws.ld(L.FI(2 * f)));
+                    ws.st(L.FI(2 * (f - 1) + 1), ws.ld(L.FI(2 * f + 1)));
+                }
+                slot = cap - 1;
+            } else {
+                ++nf;
+            }
+            ws.st(L.FI(2 * slot), ((T)1 - gamma_theta) * thetak);
+            ws.st(L.FI(2 * slot + 1), phik - gamma_phi * thetak);
+        }
+        set_sc(SC_NFILTER, (T)nf);
+        set_sc(SC_ACCA, alpha);  // applied by the next begin phase
+        set_sc(SC_ACCZ, sc(SC_AMAXZ));
+        set_sc(SC_ITER, sc(SC_ITER) + 1);
+        return 0;
+    }
+
+    // The whole solve of one problem: the phases in sequence.  Between phases the
+    // state is re-read from the workspace; the compiler barrier stops the compiler
+    // from forwarding values across phases, so each phase is register-allocated on
+    // its own (fused, their live ranges exceed the 512-register file).
+    MPCG_HD static void phase_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" ::: "memory");
+#endif
+    }
+    MPCG_HD IpmResult solve() {
+        phase_init0();
+        phase_fence();
+        phase_newton(1);
+        phase_fence();
+        phase_direction(1);
+        phase_fence();
+        phase_init1();
+        for (;;) {
+            phase_fence();
+            if (phase_begin()) break;
+            phase_fence();
+            if (phase_newton(0)) break;
+            phase_fence();
+            phase_direction(0);
+            phase_fence();
+            if (phase_linesearch()) break;
+        }
+        phase_fence();
+        restore();
+        return result();
+    }
+
+    MPCG_HD IpmResult result() const {
+        IpmResult r;
+        r.status = (int32_t)sc(SC_STATUS);
+        r.iters = (int32_t)sc(SC_ITER);
+        r.obj = 0.0;
+        r.kkt_inf = (double)sc(SC_KKT);
+        return r;
     }
 
     // Final point with honor_original_bounds projection; objective at that point.

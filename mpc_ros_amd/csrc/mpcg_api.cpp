@@ -34,6 +34,8 @@ struct mpcg_handle {
     // staging buffers for mpcg_solve (host pointers)
     double* d_io = nullptr;
     size_t io_bytes = 0;
+    mpcg::DriverCtx drv;  // device active counter, pinned readback slots, events
+    int strategy = MPCG_STRATEGY_AUTO;
 };
 
 extern "C" {
@@ -185,6 +187,14 @@ int mpcg_create(int device, mpcg_handle** out) {
         return hip_fail(e, "hipStreamCreate");
     }
     mpcg_params_plugin_default(&h->params);
+    e = hipMalloc((void**)&h->drv.d_active, sizeof(int));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->drv.h_active, 2 * sizeof(int), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drv.ev[0], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drv.ev[1], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        mpcg_destroy(h);
+        return hip_fail(e, "driver buffers");
+    }
     *out = h;
     return 0;
 }
@@ -195,6 +205,10 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->ws) hipFree(h->ws);
     if (h->d_io) hipFree(h->d_io);
+    if (h->drv.d_active) hipFree(h->drv.d_active);
+    if (h->drv.h_active) hipHostFree(h->drv.h_active);
+    for (hipEvent_t ev : h->drv.ev)
+        if (ev) hipEventDestroy(ev);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -235,6 +249,27 @@ int mpcg_reserve(mpcg_handle* h, int64_t B) {
     return ensure_ws(h, B);
 }
 
+// 160 KiB of LDS per CU; one wavefront's problem must fit with room for a second
+static const size_t kWideLdsMax = 64 * 1024;
+
+static int resolve_strategy(const mpcg_handle* h) {
+    if (h->strategy != MPCG_STRATEGY_AUTO) return h->strategy;
+    const mpcg::IpmParams P = to_ipm(h->params);
+    return (P.N <= 64 && mpcg::wide_lds_bytes(P) <= kWideLdsMax) ? MPCG_STRATEGY_WAVE : MPCG_STRATEGY_LANE;
+}
+
+int mpcg_set_strategy(mpcg_handle* h, int32_t strategy) {
+    if (!h) return fail(-1, "null handle");
+    if (strategy < MPCG_STRATEGY_AUTO || strategy > MPCG_STRATEGY_WAVE) return fail(-1, "unknown strategy");
+    h->strategy = strategy;
+    return 0;
+}
+
+int mpcg_get_strategy(const mpcg_handle* h) {
+    if (!h) return fail(-1, "null handle");
+    return resolve_strategy(h);
+}
+
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream) {
     if (!h) return fail(-1, "null handle");
@@ -245,11 +280,20 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
     if (rc) return rc;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
+    const mpcg::IpmParams P = to_ipm(h->params);
+    const int strat = resolve_strategy(h);
+    if (strat == MPCG_STRATEGY_WAVE) {
+        if (P.N > 64 || mpcg::wide_lds_bytes(P) > kWideLdsMax)
+            return fail(-1, "strategy WAVE needs steps <= 64 and the problem state within 64 KiB of LDS");
+        e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, s);
+        if (e != hipSuccess) return hip_fail(e, "wide solve launch");
+        return 0;
+    }
     rc = ensure_ws(h, B);
     if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
-    e = mpcg::launch_ipm_solve(to_ipm(h->params), B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,
-                               h->ws, s);
+    e = mpcg::launch_ipm_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,
+                               h->ws, h->drv, s);
     if (e != hipSuccess) return hip_fail(e, "ipm_solve_kernel launch");
     return 0;
 }

@@ -9,9 +9,25 @@
 
 namespace mpcg {
 
+// Host-side state of the iteration driver (owned by the handle).
+struct DriverCtx {
+    int* d_active = nullptr;   // device counter of problems still iterating
+    int* h_active = nullptr;   // 2 pinned host slots
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int chunk = 8;             // iterations launched between two counter reads
+};
+
+// Queue the whole solve on `stream`.  Returns once every problem has terminated
+// (the host polls the device counter once per chunk of iterations); the outputs
+// are written by the last kernel queued on `stream`.
 hipError_t launch_ipm_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                             double* traj, int32_t* status, double* obj, int32_t* iters, double* ws,
-                            hipStream_t stream);
+                            DriverCtx& ctx, hipStream_t stream);
+
+// One problem per wavefront (mpcg_wide.hip): LDS bytes per problem, launch.
+size_t wide_lds_bytes(const IpmParams& P);
+hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
+                             double* traj, int32_t* status, double* obj, int32_t* iters, hipStream_t stream);
 
 }  // namespace mpcg
 #endif

@@ -1,0 +1,80 @@
+// mpc_ros_amd/csrc/wave_dev.h -- CDNA4 wavefront context of the wide solver (wide_core.h).
+//
+// Lane index, the wavefront's LDS base, and the cross-lane primitives:
+//   sync()          order LDS accesses across lanes of the wavefront.  LDS
+//                   instructions of one wavefront execute in issue order, so a
+//                   compiler barrier (wave-scope fence) is all that is needed;
+//   bcast8<q>(v)    lane q of the lane's group of 8 (ds_swizzle bit mode, no LDS memory);
+//   rpart<s>(v)     partner of reduction step s: xor 1, xor 2 (DPP quad_perm), mirror
+//                   within 8, mirror within 16 (DPP row_half_mirror / row_mirror),
+//                   xor 16 (ds_swizzle), xor 32 (ds_bpermute).  Pairs are symmetric, so
+//                   a commutative op leaves every lane with identical bits;
+//   up1(v)          value of lane t-1 (lane 0: its own);
+//   any(b), uni(i)  wave vote, wave-uniform (scalar) copy of lane 0's value;
+//   ld2(i, a, b)    16-byte LDS load of two consecutive doubles (i even).
+#ifndef MPCG_WAVE_DEV_H
+#define MPCG_WAVE_DEV_H
+
+#include <hip/hip_runtime.h>
+
+namespace mpcg {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MPCG_LDS __attribute__((address_space(3)))
+#else
+#define MPCG_LDS
+#endif
+
+struct DevWaveBase {
+    typedef MPCG_LDS double ldsT;
+    typedef MPCG_LDS double2 ldsT2;
+    int t;
+    ldsT* S;
+
+    __device__ __forceinline__ void sync() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __device__ __forceinline__ void ld2(int i, double& a, double& b) const {
+        const double2 v = *(const ldsT2*)(S + i);
+        a = v.x;
+        b = v.y;
+    }
+    template <int pat>
+    __device__ __forceinline__ static double swz(double v) {
+        const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+        const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+        return __hiloint2double(hi, lo);
+    }
+    template <int ctrl>
+    __device__ __forceinline__ static double dpp(double v) {
+        const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
+        return __hiloint2double(hi, lo);
+    }
+    // ds_swizzle bit mode: lane = ((lane & and) | or) ^ xor within 32 lanes
+    template <int q>
+    __device__ __forceinline__ double bcast8(double v) const {
+        return swz<0x18 | (q << 5)>(v);
+    }
+    template <int s>
+    __device__ __forceinline__ double rpart(double v) const {
+        if (s == 0) return dpp<0xB1>(v);           // quad_perm [1,0,3,2]
+        if (s == 1) return dpp<0x4E>(v);           // quad_perm [2,3,0,1]
+        if (s == 2) return dpp<0x141>(v);          // row_half_mirror
+        if (s == 3) return dpp<0x140>(v);          // row_mirror
+        if (s == 4) return swz<0x1F | (0x10 << 10)>(v);  // xor 16
+        return __shfl_xor(v, 32, 64);
+    }
+    __device__ __forceinline__ double up1(double v) const { return __shfl_up(v, 1, 64); }
+    __device__ __forceinline__ bool any(bool b) const { return __any(b); }
+    __device__ __forceinline__ int uni(int v) const { return __builtin_amdgcn_readfirstlane(v); }
+};
+
+struct DevWave : DevWaveBase {
+    __device__ __forceinline__ void mark(int) const {}
+};
+
+}  // namespace mpcg
+#endif

@@ -1,0 +1,1025 @@
+// mpc_ros_amd/csrc/wide_core.h -- the same interior-point solve, one problem per wavefront.
+//
+// ipm_core.h runs one problem per lane: a wavefront carries 64 problems and takes as
+// long as the slowest of them, and a lone wavefront issues every FP64 instruction of
+// its iteration itself (~1M cycles per iteration).  The iteration counts of this NLP
+// are heavy-tailed (infinity set: mean 14, p99 35, max >130), so at one problem per
+// lane the batch time is set by a handful of slow problems.  This solver spreads one
+// problem over the 64 lanes of a wavefront instead:
+//
+//   * stage-parallel sweeps (accept, statistics, trial points, multipliers, step
+//     statistics): lane k owns stage k (N <= 64); sums/extrema by xor-butterflies;
+//     the dynamics value F(s_k, u_k) moves to lane k+1 by one lane shift;
+//   * the Riccati recursion: lane (i, j) = (t >> 3, t & 7) owns entry (i, j) of the
+//     8x8 cost-to-go matrix; per stage one dense 8x8 product M = P' [A | B | d]
+//     (entry per lane), the 2x8 projection B^T M by 16 lanes, and the update
+//     P = Q + A^T M + S^T K (entry per lane); the stage data that does not depend on
+//     P (linearisation, barrier Hessian, gradients) is computed for all stages in
+//     parallel before the sweep;
+//   * the forward recursion of the step (8-vector) runs replicated in every lane.
+//
+// The problem state (iterate, multipliers, step, Riccati records, filter) lives in
+// the wavefront's LDS for the whole solve.  Per-problem scalars (mu, tau, filter
+// size, ...) are wave-uniform; every control decision is taken on butterfly-reduced
+// values, which are bitwise identical in all lanes.
+//
+// Numerically this is ipm_core.h's algorithm with the same constants and formulas;
+// only the order of some sums differs (tree instead of sequential), i.e. results
+// agree with the one-problem-per-lane solver and with the oracle to rounding.
+//
+// The wavefront context WV supplies the lane index, the LDS base, the cross-lane
+// primitives and mark(phase) (a no-op except in the phase-timing build tools/wide_prof.hip): the device implementation is in mpcg_wide.hip, a host emulation with
+// 64 threads in tests/native/wide_host_check.cpp.
+#ifndef MPCG_WIDE_CORE_H
+#define MPCG_WIDE_CORE_H
+
+#include "ipm_core.h"
+
+namespace mpcg {
+
+// LDS layout of one problem (doubles).
+struct WideLayout {
+    int N, cap;
+    static constexpr int SS = 44;  // stage table stride
+    // stage table entries
+    static constexpr int SA = 0;    // a[7]: non-trivial entries of A_k (Lin::jac)
+    static constexpr int SDT = 7;   // dt
+    static constexpr int SD = 8;    // d[6]: F(s_k, u_k) - s_{k+1} (Newton mode)
+    static constexpr int SKF = 14;  // kff[2]
+    static constexpr int SQD = 16;  // diag of the stage Hessian (6 states, 2 controls = R)
+    static constexpr int SQV = 24;  // gradient q (6) and r (2)
+    static constexpr int SCV = 32;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
+    static constexpr int SCC = 37;  // rate coupling C0 C1
+    static constexpr int SZERO = 39, SONE = 40, SMONE = 41;  // constants 0, 1, -1
+    MPCG_HD int W(int k) const { return 8 * k; }
+    MPCG_HD int ZL(int k) const { return 8 * N + 8 * k; }
+    MPCG_HD int ZU(int k) const { return 16 * N + 8 * k; }
+    MPCG_HD int DW(int k) const { return 24 * N + 8 * k; }
+    MPCG_HD int Y(int k) const { return 32 * N + 8 * k; }
+    MPCG_HD int YP(int k) const { return 40 * N + 8 * k; }
+    MPCG_HD int PM(int k) const { return 48 * N + 36 * k; }  // packed symmetric 8x8 (pidx)
+    MPCG_HD int PV(int k) const { return 84 * N + 8 * k; }
+    MPCG_HD int KR(int k) const { return 92 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
+    MPCG_HD int ST(int k) const { return 108 * N + SS * k; }
+    // scratch of the Riccati sweep: M[64] | Z[16] C0 C1 0
+    MPCG_HD int SCR() const { return 152 * N; }
+    MPCG_HD int RSC() const { return 152 * N + 88; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int FI() const { return 152 * N + 104; }
+    MPCG_HD int total() const { return 152 * N + 104 + 2 * cap; }
+};
+
+template <class WV>
+struct WideSolver {
+    typedef double T;
+    const IpmParams P;
+    const IpmProblem<T> pr;
+    WV wv;
+    WideLayout L;
+    int N, t;
+    T dt;
+    T sl, su, wl, wu, al, au, sl0, su0, wl0, wu0, al0, au0;
+    T sf;
+    T mu, tau;
+    // statistics of the current iterate
+    T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
+    // line-search / iteration state
+    T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt;
+    int iter, nf, status;
+
+    MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_)
+        : P(P_), pr(pr_), wv(wv_), L{P_.N, P_.filter_cap}, N(P_.N), t(wv_.t), dt((T)P_.dt) {}
+
+    // ------------------------------------------------------------ LDS helpers
+    MPCG_HD T ld(int i) const { return wv.S[i]; }
+    MPCG_HD void st(int i, T v) const { wv.S[i] = v; }
+    template <int n>
+    MPCG_HD void ldn(int i, T* v) const {
+#pragma unroll
+        for (int j = 0; j < n; ++j) v[j] = wv.S[i + j];
+    }
+
+    // ------------------------------------------------------ wave reductions
+    // Six pairwise steps over symmetric lane pairs (WV::rpart): every lane ends with
+    // the same bits.  Several reductions run interleaved step by step.
+    enum { RSUM = 0, RMAX = 1, RMIN = 2 };
+    template <int s, int n>
+    MPCG_HD void rstep(T* v, const int* op) {
+        T o[n];
+#pragma unroll
+        for (int q = 0; q < n; ++q) o[q] = wv.template rpart<s>(v[q]);
+#pragma unroll
+        for (int q = 0; q < n; ++q)
+            v[q] = op[q] == RSUM ? v[q] + o[q] : (op[q] == RMAX ? tmax(v[q], o[q]) : tmin(v[q], o[q]));
+    }
+    template <int n>
+    MPCG_HD void reduce(T* v, const int* op) {
+        rstep<0, n>(v, op);
+        rstep<1, n>(v, op);
+        rstep<2, n>(v, op);
+        rstep<3, n>(v, op);
+        rstep<4, n>(v, op);
+        rstep<5, n>(v, op);
+    }
+    MPCG_HD T rsum(T v) {
+        const int op[1] = {RSUM};
+        reduce<1>(&v, op);
+        return v;
+    }
+    MPCG_HD T rmax(T v) {
+        const int op[1] = {RMAX};
+        reduce<1>(&v, op);
+        return v;
+    }
+    // 16-byte LDS load of two consecutive doubles (i even)
+    MPCG_HD void ld2(int i, T& a, T& b) const { wv.ld2(i, a, b); }
+    template <int n>
+    MPCG_HD void ldv(int i, T* v) const {
+#pragma unroll
+        for (int j = 0; j < n; j += 2) wv.ld2(i + j, v[j], v[j + 1]);
+    }
+
+    // ------------------------------------------------------ model helpers
+    // row scale of dynamics row s into stage k (1 for the initial-state rows), from LDS
+    MPCG_HD T rowscale(int s, int k) const { return ld(L.RSC() + (k == 0 ? 12 : (k == 1 ? s : 6 + s))); }
+    MPCG_HD T vlo(int j) const { return j < 6 ? sl : (j == 6 ? wl : al); }
+    MPCG_HD T vhi(int j) const { return j < 6 ? su : (j == 6 ? wu : au); }
+    MPCG_HD T cost_state(const T* s) const {
+        const T e1 = s[4] - (T)P.ref_cte, e2 = s[5] - (T)P.ref_eth, e3 = s[3] - (T)P.ref_v;
+        return (T)P.w_cte * e1 * e1 + (T)P.w_eth * e2 * e2 + (T)P.w_v * e3 * e3;
+    }
+    MPCG_HD void grad_state(const T* s, T* g) const {
+        g[0] = 0; g[1] = 0; g[2] = 0;
+        g[3] = (T)(2.0 * P.w_v) * (s[3] - (T)P.ref_v);
+        g[4] = (T)(2.0 * P.w_cte) * (s[4] - (T)P.ref_cte);
+        g[5] = (T)(2.0 * P.w_eth) * (s[5] - (T)P.ref_eth);
+    }
+    MPCG_HD T hess_state(int j) const {
+        return j == 3 ? (T)(2.0 * P.w_v) : (j == 4 ? (T)(2.0 * P.w_cte) : (j == 5 ? (T)(2.0 * P.w_eth) : (T)0));
+    }
+    MPCG_HD void grad_ctrl(int k, const T* um, const T* u, const T* up, T* g) const {
+        g[0] = (T)(2.0 * P.w_w) * u[0];
+        g[1] = (T)(2.0 * P.w_a) * u[1];
+        if (k >= 1) {
+            g[0] += (T)(2.0 * P.w_dw) * (u[0] - um[0]);
+            g[1] += (T)(2.0 * P.w_da) * (u[1] - um[1]);
+        }
+        if (k <= N - 3) {
+            g[0] -= (T)(2.0 * P.w_dw) * (up[0] - u[0]);
+            g[1] -= (T)(2.0 * P.w_da) * (up[1] - u[1]);
+        }
+    }
+    MPCG_HD T hess_ctrl(int k, int j) const {
+        const double wd = j == 0 ? P.w_dw : P.w_da;
+        const double w = j == 0 ? P.w_w : P.w_a;
+        return (T)(2.0 * w + 2.0 * wd * ((k >= 1 ? 1 : 0) + (k <= N - 3 ? 1 : 0)));
+    }
+    MPCG_HD T cost_ctrl(int k, const T* u, const T* up) const {
+        T f = (T)P.w_w * u[0] * u[0] + (T)P.w_a * u[1] * u[1];
+        if (k <= N - 3)
+            f += (T)P.w_dw * (up[0] - u[0]) * (up[0] - u[0]) + (T)P.w_da * (up[1] - u[1]) * (up[1] - u[1]);
+        return f;
+    }
+
+    // ------------------------------------------------------------ setup
+    // Same as IpmSolver::setup (ipm_core.h), uniform in every lane.
+    MPCG_HD void rowscales_at(const T* s, T* rs) const {
+        Lin<T> ln;
+        ln.eval(pr.c, s);
+        T m[6];
+        m[0] = tmax((T)1, tmax((T)fabs(s[3] * ln.st * dt), (T)fabs(ln.ct * dt)));
+        m[1] = tmax((T)1, tmax((T)fabs(s[3] * ln.ct * dt), (T)fabs(ln.st * dt)));
+        m[2] = tmax((T)1, dt);
+        m[3] = tmax((T)1, dt);
+        m[4] = tmax(tmax((T)1, (T)fabs(ln.f1)), tmax((T)fabs(ln.se * dt), (T)fabs(s[3] * ln.ce * dt)));
+        m[5] = tmax((T)1, dt);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) rs[j] = m[j] > (T)100 ? (T)100 / m[j] : (T)1;
+    }
+    MPCG_HD void bounds_only() {
+        const T rl = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.bound));
+        sl0 = (T)-P.bound; su0 = (T)P.bound; sl = sl0 - rl; su = su0 + rl;
+        const T rw = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_w));
+        wl0 = (T)-P.max_w; wu0 = (T)P.max_w; wl = wl0 - rw; wu = wu0 + rw;
+        const T rA = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_a));
+        al0 = (T)-P.max_a; au0 = (T)P.max_a; al = al0 - rA; au = au0 + rA;
+    }
+    MPCG_HD void setup() {
+        bounds_only();
+        T g[6];
+        grad_state(pr.init, g);
+        T gm = tmax((T)fabs(g[3]), tmax((T)fabs(g[4]), (T)fabs(g[5])));
+        if (N >= 2) {
+            const T z[6] = {0, 0, 0, 0, 0, 0};
+            grad_state(z, g);
+            gm = tmax(gm, tmax((T)fabs(g[3]), tmax((T)fabs(g[4]), (T)fabs(g[5]))));
+        }
+        sf = gm > (T)100 ? (T)100 / gm : (T)1;
+        T ra[6], rb[6];
+        rowscales_at(pr.init, ra);
+        const T z6[6] = {0, 0, 0, 0, 0, 0};
+        rowscales_at(z6, rb);
+        if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                st(L.RSC() + j, ra[j]);
+                st(L.RSC() + 6 + j, rb[j]);
+            }
+            st(L.RSC() + 12, 1);
+        }
+    }
+    MPCG_HD T push(T v, T lo, T hi) const {
+        const T pl = tmin((T)0.01 * tmax((T)1, (T)fabs(lo)), (T)0.01 * (hi - lo));
+        const T pu = tmin((T)0.01 * tmax((T)1, (T)fabs(hi)), (T)0.01 * (hi - lo));
+        if (v < lo + pl) v = lo + pl;
+        if (v > hi - pu) v = hi - pu;
+        return v;
+    }
+    MPCG_HD void init_point() {
+        if (t < N) {
+            const int k = t;
+            for (int j = 0; j < 8; ++j) {
+                st(L.W(k) + j, push((j < 6 && k == 0) ? pr.init[j] : (T)0, vlo(j), vhi(j)));
+                st(L.ZL(k) + j, 1);
+                st(L.ZU(k) + j, 1);
+                st(L.Y(k) + j, 0);
+                st(L.YP(k) + j, 0);
+                st(L.DW(k) + j, 0);
+            }
+        }
+    }
+
+    // ------------------------------------------------ accept + statistics
+    MPCG_HD void accept_one(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun) const {
+        const T ksig = (T)1e10, iksig = (T)1e-10;
+        const T rdl = rcp(w - lo), rdu = rcp(hi - w);
+        const T dzl = mu * rdl - zl - zl * rdl * dwv;
+        const T dzu = mu * rdu - zu + zu * rdu * dwv;
+        *wn = w + alpha * dwv;
+        const T rs2 = rcp(*wn - lo), ru2 = rcp(hi - *wn);
+        const T a = zl + amax_z * dzl, b = zu + amax_z * dzu;
+        *zln = tmax(tmin(a, ksig * mu * rs2), mu * rs2 * iksig);
+        *zun = tmax(tmin(b, ksig * mu * ru2), mu * ru2 * iksig);
+    }
+
+    MPCG_HD void stats(bool acc, T alpha, T amax_z) {
+        wv.sync();
+        if (acc && t < N) {
+            const int k = t;
+            const bool last = k == N - 1;
+            T w[8], dw[8], zl[8], zu[8], y[6], yp[6];
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.DW(k), dw);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            ldn<6>(L.YP(k), yp);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (!(last && j >= 6)) {
+                    T wn, zln, zun;
+                    accept_one(w[j], dw[j], zl[j], zu[j], vlo(j), vhi(j), alpha, amax_z, &wn, &zln, &zun);
+                    st(L.W(k) + j, wn);
+                    st(L.ZL(k) + j, zln);
+                    st(L.ZU(k) + j, zun);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(L.Y(k) + j, y[j] + alpha * (yp[j] - y[j]));
+        }
+        wv.sync();
+        T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
+          lg = 0;
+        T Fk[6] = {0, 0, 0, 0, 0, 0};
+        T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[7];
+        const int k = t;
+        const bool act = t < N, last = k == N - 1;
+        if (act) {
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                up[0] = ld(L.W(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7);
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                ln.jac(w, dt, a);
+                ln.next(w, w + 6, dt, Fk);
+            }
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+        }
+        T Fprev[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Fprev[j] = wv.up1(Fk[j]);
+        if (act) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                const T rsc = rowscale(j, k);
+                const T cs = rsc * c;
+                th += fabs(cs);
+                pinf = tmax(pinf, (T)fabs(cs));
+                puns = tmax(puns, (T)fabs(c));
+                ly += fabs(y[j]) * rcp(rsc);
+            }
+            f = cost_state(w);
+            T g[6], at[6] = {0, 0, 0, 0, 0, 0}, gu[2] = {0, 0};
+            grad_state(w, g);
+            if (!last) {
+                AT_mul(a, yn, at);
+                grad_ctrl(k, um, w + 6, up, gu);
+                f += cost_ctrl(k, w + 6, up);
+            }
+            const T btw = dt * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T gj = j < 6 ? sf * g[j] + y[j] - at[j] : sf * gu[j - 6] - (j == 6 ? btw : bta);
+                    const T rd = gj - zl[j] + zu[j];
+                    dinf = tmax(dinf, (T)fabs(rd));
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    slackprod *= dl * du;
+                    const T p1 = dl * zl[j], p2 = du * zu[j];
+                    c0 = tmax(c0, tmax((T)fabs(p1), (T)fabs(p2)));
+                    mn = tmin(mn, tmin(p1, p2));
+                    mx = tmax(mx, tmax(p1, p2));
+                    lz += fabs(zl[j]) + fabs(zu[j]);
+                }
+            }
+            lg = log(slackprod);
+        }
+        T v[11] = {f, th, pinf, puns, dinf, c0, mn, mx, ly, lz, lg};
+        const int op[11] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM};
+        reduce<11>(v, op);
+        fval = v[0];
+        theta = v[1];
+        prim_inf = v[2];
+        prim_uns = v[3];
+        dual_inf = v[4];
+        compl0 = v[5];
+        pmin = v[6];
+        pmax = v[7];
+        l1y = v[8];
+        l1z = v[9];
+        logsum = v[10];
+        wv.mark(0);
+    }
+
+    // ------------------------------------------------------- Riccati backward
+    // Stage data that does not depend on the cost-to-go, all stages in parallel.
+    MPCG_HD void precompute(int mode, T delta_w) {
+        if (t >= N) return;
+        const int k = t;
+        const bool last = k == N - 1;
+        const int sb = L.ST(k);
+        T w[8], zl[8], zu[8];
+        ldn<8>(L.W(k), w);
+        ldn<8>(L.ZL(k), zl);
+        ldn<8>(L.ZU(k), zu);
+        T g[6];
+        grad_state(w, g);
+        T a[7] = {0, 0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
+        T cv[5] = {0, 0, 0, 0, 0};
+        if (!last) {
+            Lin<T> ln;
+            ln.eval(pr.c, w);
+            ln.jac(w, dt, a);
+            if (mode == 0) {
+                T F[6], wn[6], cy[6];
+                ln.next(w, w + 6, dt, F);
+                ldn<6>(L.W(k + 1), wn);
+                ldn<6>(L.Y(k + 1), cy);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) d[j] = F[j] - wn[j];
+                const T v = w[3];
+                cv[0] = -cy[4] * ln.f2;                                   // Q00
+                cv[1] = cy[0] * v * ln.ct * dt + cy[1] * v * ln.st * dt;  // Q22
+                cv[2] = cy[0] * ln.st * dt - cy[1] * ln.ct * dt;          // Q32
+                cv[3] = cy[4] * v * ln.se * dt;                           // Q55
+                cv[4] = -cy[4] * ln.ce * dt;                              // Q53
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+        st(sb + WideLayout::SDT, dt);
+        st(sb + WideLayout::SZERO, 0);
+        st(sb + WideLayout::SONE, 1);
+        st(sb + WideLayout::SMONE, -1);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, d[j]);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cv[j]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            T qd, qv;
+            if (mode == 0) {
+                const T rdl = rcp(w[j] - sl), rdu = rcp(su - w[j]);
+                qd = sf * hess_state(j) + zl[j] * rdl + zu[j] * rdu + delta_w;
+                qv = sf * g[j] - mu * rdl + mu * rdu;
+            } else {
+                qd = 1;
+                qv = sf * g[j] - zl[j] + zu[j];
+            }
+            st(sb + WideLayout::SQD + j, qd);
+            st(sb + WideLayout::SQV + j, qv);
+        }
+        T R[2] = {0, 0}, r[2] = {0, 0}, C0 = 0, C1 = 0;
+        if (!last) {
+            T um[2] = {0, 0}, up[2], gu[2];
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            up[0] = ld(L.W(k + 1) + 6);
+            up[1] = ld(L.W(k + 1) + 7);
+            grad_ctrl(k, um, w + 6, up, gu);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (mode == 0) {
+                    const T rdl = rcp(w[6 + j] - vlo(6 + j)), rdu = rcp(vhi(6 + j) - w[6 + j]);
+                    R[j] = sf * hess_ctrl(k, j) + zl[6 + j] * rdl + zu[6 + j] * rdu + delta_w;
+                    r[j] = sf * gu[j] - mu * rdl + mu * rdu;
+                } else {
+                    R[j] = 1;
+                    r[j] = sf * gu[j] - zl[6 + j] + zu[6 + j];
+                }
+            }
+            if (mode == 0 && k >= 1) {
+                C0 = -sf * (T)(2.0 * P.w_dw);
+                C1 = -sf * (T)(2.0 * P.w_da);
+            }
+        }
+        st(sb + WideLayout::SQD + 6, R[0]);
+        st(sb + WideLayout::SQD + 7, R[1]);
+        st(sb + WideLayout::SQV + 6, r[0]);
+        st(sb + WideLayout::SQV + 7, r[1]);
+        st(sb + WideLayout::SCC + 0, C0);
+        st(sb + WideLayout::SCC + 1, C1);
+    }
+
+    // Stage-table offset of G[m][s], G = [A_hat cols 0,1,2,3,5 | B_hat cols w,a | d]
+    // (s < 0: a zero column).  A_hat = dF/ds with rows 6,7 (u_{k-1}) zero.
+    MPCG_HD static int goff(int s, int m) {
+        typedef WideLayout W_;
+        const int Z = W_::SZERO, O = W_::SONE, A = W_::SA, D = W_::SD;
+        int o = Z;
+        o = (s == 0) ? (m == 0 ? O : (m == 4 ? A + 4 : Z)) : o;
+        o = (s == 1) ? (m == 1 ? O : (m == 4 ? W_::SMONE : Z)) : o;
+        o = (s == 2) ? (m == 0 ? A + 0 : (m == 1 ? A + 2 : (m == 2 ? O : Z))) : o;
+        o = (s == 3) ? (m == 0 ? A + 1 : (m == 1 ? A + 3 : (m == 3 ? O : (m == 4 ? A + 5 : Z)))) : o;
+        o = (s == 4) ? (m == 4 ? A + 6 : (m == 5 ? O : Z)) : o;
+        // B_hat: w -> dt e2 + dt e5 + e6 ; a -> dt e3 + e7
+        o = (s == 5) ? ((m == 2 || m == 5) ? W_::SDT : (m == 6 ? O : Z)) : o;
+        o = (s == 6) ? (m == 3 ? W_::SDT : (m == 7 ? O : Z)) : o;
+        o = (s == 7) ? (m < 6 ? D + m : Z) : o;
+        return o;
+    }
+    // slot of augmented-state column j among the A_hat columns of G (-1: zero column)
+    MPCG_HD static int aslot(int j) { return j < 4 ? j : (j == 5 ? 4 : -1); }
+
+    MPCG_HD bool riccati(int mode, T delta_w) {
+        wv.sync();
+        precompute(mode, delta_w);
+        typedef WideLayout W_;
+        const int i = t >> 3, j = t & 7;
+        const int si = aslot(i), sj = aslot(j);
+        const int sm = L.SCR();
+        // per-lane stage-table offsets: G column j, A_hat column i
+        int go[8], ao[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            go[q] = goff(j, q);
+            ao[q] = goff(si, q);
+        }
+        // M columns sj and si (clamped, masked by hj / hi) and the rate-coupling entries of S_tilde
+        const bool hj = sj >= 0, hi = si >= 0;
+        const int mj = sm + (hj ? sj : 0), mi = sm + (hi ? si : 0);
+        const int c0j = j == 6 ? W_::SCC : W_::SZERO, c1j = j == 7 ? W_::SCC + 1 : W_::SZERO;
+        const int c0i = i == 6 ? W_::SCC : W_::SZERO, c1i = i == 7 ? W_::SCC + 1 : W_::SZERO;
+        // Q_hat(i, j): diagonal, constraint curvature
+        const int q1 = (i == j && i < 6) ? W_::SQD + i : W_::SZERO;
+        int q2 = W_::SZERO;
+        q2 = (i == 0 && j == 0) ? W_::SCV + 0 : q2;
+        q2 = (i == 2 && j == 2) ? W_::SCV + 1 : q2;
+        q2 = ((i == 3 && j == 2) || (i == 2 && j == 3)) ? W_::SCV + 2 : q2;
+        q2 = (i == 5 && j == 5) ? W_::SCV + 3 : q2;
+        q2 = ((i == 5 && j == 3) || (i == 3 && j == 5)) ? W_::SCV + 4 : q2;
+        const int qv = i < 6 ? W_::SQV + i : W_::SZERO;
+        const bool wr = j <= i;  // lane writes the packed record entry
+        const int pw = pidx(i, j);
+        wv.sync();
+        wv.mark(1);
+        // terminal stage; lane (i, j) keeps P(i, j) in a register from here on
+        T Pij;
+        {
+            const int sb = L.ST(N - 1);
+            Pij = ld(sb + q1);
+            if (wr) st(L.PM(N - 1) + pw, Pij);
+            if (j == 0) st(L.PV(N - 1) + i, ld(sb + qv));
+        }
+        for (int k = N - 2; k >= 0; --k) {
+            const int sb = L.ST(k);
+            // row i of P' from the 8 lanes of the row; column j of G from the stage table
+            T pr_[8], g[8];
+            pr_[0] = wv.template bcast8<0>(Pij);
+            pr_[1] = wv.template bcast8<1>(Pij);
+            pr_[2] = wv.template bcast8<2>(Pij);
+            pr_[3] = wv.template bcast8<3>(Pij);
+            pr_[4] = wv.template bcast8<4>(Pij);
+            pr_[5] = wv.template bcast8<5>(Pij);
+            pr_[6] = wv.template bcast8<6>(Pij);
+            pr_[7] = wv.template bcast8<7>(Pij);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) g[q] = ld(sb + go[q]);
+            wv.sync();
+            // M = P' G, entry (i, j) per lane; column 7 adds p' (h = P' d + p')
+            T m0 = (j == 7) ? ld(L.PV(k + 1) + i) : (T)0, m1 = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                m0 += pr_[q] * g[q];
+                m1 += pr_[q + 1] * g[q + 1];
+            }
+            st(sm + t, m0 + m1);
+            wv.sync();
+            // every lane reads the entries of M it needs: columns sj (all rows), 7 (all rows),
+            // the B_hat rows (2,3,5,6,7) of columns 5, 6 and si
+            T mc[8], m7[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                mc[q] = ld(mj + 8 * q);
+                m7[q] = ld(sm + 8 * q + 7);
+            }
+            const T m25 = ld(sm + 21), m55 = ld(sm + 45), m65 = ld(sm + 53);
+            const T m26 = ld(sm + 22), m56 = ld(sm + 46), m66 = ld(sm + 54), m36 = ld(sm + 30), m76 = ld(sm + 62);
+            const T mi2 = ld(mi + 16), mi3 = ld(mi + 24), mi5 = ld(mi + 40), mi6 = ld(mi + 48), mi7 = ld(mi + 56);
+            T qd6, qd7, qv6, qv7;
+            ld2(sb + W_::SQD + 6, qd6, qd7);
+            ld2(sb + W_::SQV + 6, qv6, qv7);
+            T c[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c[q] = ld(sb + ao[q]);
+            const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
+            const T qh = ld(sb + q1) + ld(sb + q2);
+            const T qvi = ld(sb + qv);
+            // R_tilde = R + B^T P' B, r_tilde = r + B^T h, S_tilde = B^T P' A (+ rate coupling)
+            const T Rt00 = qd6 + (dt * (m25 + m55) + m65);
+            const T Rt01 = dt * (m26 + m56) + m66;
+            const T Rt11 = qd7 + (dt * m36 + m76);
+            const T det = Rt00 * Rt11 - Rt01 * Rt01;
+            if (wv.uni(!(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11))) {
+                wv.mark(2);
+                return false;
+            }
+            const T rt0 = qv6 + (dt * (m7[2] + m7[5]) + m7[6]);
+            const T rt1 = qv7 + (dt * m7[3] + m7[7]);
+            const T rdet = rcp(det);
+            const T i00 = Rt11 * rdet, i01 = -Rt01 * rdet, i11 = Rt00 * rdet;
+            const T s0j = hj ? dt * (mc[2] + mc[5]) + mc[6] : cc0j;
+            const T s1j = hj ? dt * mc[3] + mc[7] : cc1j;
+            const T s0i = hi ? dt * (mi2 + mi5) + mi6 : cc0i;
+            const T s1i = hi ? dt * mi3 + mi7 : cc1i;
+            const T K0 = -(i00 * s0j + i01 * s1j);
+            const T K1 = -(i01 * s0j + i11 * s1j);
+            const T kf0 = -(i00 * rt0 + i01 * rt1);
+            const T kf1 = -(i01 * rt0 + i11 * rt1);
+            // (A_hat^T M)(i, j) and (A_hat^T h)(i)
+            T a0 = 0, a1 = 0, h0 = 0, h1 = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                a0 += c[q] * mc[q];
+                a1 += c[q + 1] * mc[q + 1];
+                h0 += c[q] * m7[q];
+                h1 += c[q + 1] * m7[q + 1];
+            }
+            Pij = qh + (hj ? a0 + a1 : (T)0) + s0i * K0 + s1i * K1;
+            if (wr) st(L.PM(k) + pw, Pij);
+            if (j == 0) st(L.PV(k) + i, qvi + (h0 + h1) + s0i * kf0 + s1i * kf1);
+            if (i == 0) {
+                st(L.KR(k) + j, K0);
+                st(L.KR(k) + 8 + j, K1);
+            }
+            if (t == 0) {
+                st(sb + W_::SKF, kf0);
+                st(sb + W_::SKF + 1, kf1);
+            }
+        }
+        wv.mark(2);
+        return true;
+    }
+
+    // -------------------------------------------------------- forward pass
+    struct Fwd {
+        T amax_p, amax_z, gd, rel;
+    };
+    MPCG_HD void dir_var(T w, T zl, T zu, T lo, T hi, T gphi, T dwv, Fwd& F) const {
+        const T dl = w - lo, du = hi - w;
+        const T rdl = rcp(dl), rdu = rcp(du), rdw = rcp(dwv);
+        const T inf = (T)INFINITY;
+        F.amax_p = tmin(F.amax_p, dwv < 0 ? -tau * dl * rdw : (dwv > 0 ? tau * du * rdw : inf));
+        const T dzl = mu * rdl - zl - zl * rdl * dwv;
+        const T dzu = mu * rdu - zu + zu * rdu * dwv;
+        F.amax_z = tmin(F.amax_z, dzl < 0 ? -tau * zl * rcp(dzl) : inf);
+        F.amax_z = tmin(F.amax_z, dzu < 0 ? -tau * zu * rcp(dzu) : inf);
+        F.gd += gphi * dwv;
+        F.rel = tmax(F.rel, (T)fabs(dwv) * rcp((T)1 + (T)fabs(w)));
+    }
+
+    MPCG_HD Fwd forward(int mode) {
+        wv.sync();
+        // the step recursion, replicated in every lane; stage k+1's records are read
+        // while stage k computes
+        T ds[8];
+        {
+            T w0[6];
+            ldn<6>(L.W(0), w0);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) ds[j] = (mode == 0) ? -(w0[j] - pr.init[j]) : (T)0;
+            ds[6] = 0;
+            ds[7] = 0;
+        }
+        T K[16], kf[2], a[8], d[6];
+        ldv<16>(L.KR(0), K);
+        ldv<2>(L.ST(0) + WideLayout::SKF, kf);
+        ldv<8>(L.ST(0) + WideLayout::SA, a);
+        ldv<6>(L.ST(0) + WideLayout::SD, d);
+        for (int k = 0; k < N - 1; ++k) {
+            T Kn[16], kfn[2], an[8], dn[6];
+            const int kn = k + 1 < N - 1 ? k + 1 : k;
+            ldv<16>(L.KR(kn), Kn);
+            ldv<2>(L.ST(kn) + WideLayout::SKF, kfn);
+            ldv<8>(L.ST(kn) + WideLayout::SA, an);
+            ldv<6>(L.ST(kn) + WideLayout::SD, dn);
+            T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
+#pragma unroll
+            for (int m = 0; m < 8; m += 2) {
+                u0a += K[m] * ds[m];
+                u0b += K[m + 1] * ds[m + 1];
+                u1a += K[8 + m] * ds[m];
+                u1b += K[9 + m] * ds[m + 1];
+            }
+            const T du0 = u0a + u0b, du1 = u1a + u1b;
+            if (t == 0) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) st(L.DW(k) + j, ds[j]);
+                st(L.DW(k) + 6, du0);
+                st(L.DW(k) + 7, du1);
+            }
+            T nx6[6];
+            A_mul(a, ds, nx6);
+            nx6[2] += dt * du0;
+            nx6[3] += dt * du1;
+            nx6[5] += dt * du0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) ds[j] = nx6[j] + d[j];
+            ds[6] = du0;
+            ds[7] = du1;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) K[q] = Kn[q];
+            kf[0] = kfn[0];
+            kf[1] = kfn[1];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = an[q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) d[q] = dn[q];
+        }
+        if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(L.DW(N - 1) + j, ds[j]);
+            st(L.DW(N - 1) + 6, 0);
+            st(L.DW(N - 1) + 7, 0);
+        }
+        wv.sync();
+        wv.mark(3);
+        Fwd F{(T)1, (T)1, (T)0, (T)0};
+        if (t < N) {
+            const int k = t;
+            const bool last = k == N - 1;
+            T dsk[8];
+            ldn<6>(L.DW(k), dsk);
+            dsk[6] = k >= 1 ? ld(L.DW(k - 1) + 6) : (T)0;
+            dsk[7] = k >= 1 ? ld(L.DW(k - 1) + 7) : (T)0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                T acc0 = ld(L.PV(k) + r), acc1 = 0;
+#pragma unroll
+                for (int m = 0; m < 8; m += 2) {
+                    acc0 += ld(L.PM(k) + pidx(r, m)) * dsk[m];
+                    acc1 += ld(L.PM(k) + pidx(r, m + 1)) * dsk[m + 1];
+                }
+                st(L.YP(k) + r, -(acc0 + acc1));
+            }
+            if (mode == 0) {
+                T w[8], zl[8], zu[8], dk[8];
+                ldn<8>(L.W(k), w);
+                ldn<8>(L.ZL(k), zl);
+                ldn<8>(L.ZU(k), zu);
+                ldn<8>(L.DW(k), dk);
+                T g[6], gu[2] = {0, 0};
+                grad_state(w, g);
+                if (!last) {
+                    T um[2] = {0, 0}, up[2];
+                    if (k >= 1) {
+                        um[0] = ld(L.W(k - 1) + 6);
+                        um[1] = ld(L.W(k - 1) + 7);
+                    }
+                    up[0] = ld(L.W(k + 1) + 6);
+                    up[1] = ld(L.W(k + 1) + 7);
+                    grad_ctrl(k, um, w + 6, up, gu);
+                }
+                const int nv = last ? 6 : 8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (j < nv) {
+                        const T gj = j < 6 ? sf * g[j] : sf * gu[j - 6];
+                        const T gphi = gj - mu * rcp(w[j] - vlo(j)) + mu * rcp(vhi(j) - w[j]);
+                        dir_var(w[j], zl[j], zu[j], vlo(j), vhi(j), gphi, dk[j], F);
+                    }
+                }
+            }
+        }
+        if (mode == 0) {
+            T v[4] = {F.amax_p, F.amax_z, F.gd, F.rel};
+            const int op[4] = {RMIN, RMIN, RSUM, RMAX};
+            reduce<4>(v, op);
+            F.amax_p = v[0];
+            F.amax_z = v[1];
+            F.gd = v[2];
+            F.rel = v[3];
+        }
+        wv.mark(4);
+        return F;
+    }
+
+    // ------------------------------------------------------------ trial point
+    MPCG_HD bool trial(T alpha, T* phi, T* th) {
+        T f = 0, thv = 0, lg = 0;
+        int bad = 0;
+        T Fk[6] = {0, 0, 0, 0, 0, 0};
+        T w[8];
+        const int k = t;
+        const bool act = t < N, last = k == N - 1;
+        if (act) {
+            T cw[8], cd[8];
+            ldn<8>(L.W(k), cw);
+            ldn<8>(L.DW(k), cd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = cw[j] + alpha * cd[j];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    bad |= !((dl > 0) && (du > 0));
+                    slackprod *= dl * du;
+                }
+            }
+            lg = log(slackprod);
+            f = cost_state(w);
+            if (!last) {
+                T up[2];
+                up[0] = ld(L.W(k + 1) + 6) + alpha * ld(L.DW(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7) + alpha * ld(L.DW(k + 1) + 7);
+                f += cost_ctrl(k, w + 6, up);
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                ln.next(w, w + 6, dt, Fk);
+            }
+        }
+        T Fprev[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Fprev[j] = wv.up1(Fk[j]);
+        if (act) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                thv += fabs(rowscale(j, k) * c);
+            }
+        }
+        T v[3] = {f, thv, lg};
+        const int op[3] = {RSUM, RSUM, RSUM};
+        reduce<3>(v, op);
+        f = v[0];
+        thv = v[1];
+        lg = v[2];
+        const bool anybad = wv.any(bad != 0);
+        wv.mark(5);
+        *phi = sf * f - mu * lg;
+        *th = thv;
+        return !anybad && isfinite((double)*phi);
+    }
+
+    // ------------------------------------------------------------ phases
+    MPCG_HD void init() {
+        setup();
+        init_point();
+        mu = (T)P.mu_init;
+        tau = tmax((T)0.99, (T)1 - (T)P.mu_init);
+        status = 0;
+        // least-squares multipliers (constr_mult_init_max 1000)
+        const bool ok = riccati(1, (T)0);
+        T ymax = 0;
+        if (ok) {
+            forward(1);
+            wv.sync();
+            T m = 0;
+            if (t < N) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) * rcp(rowscale(j, t))));
+            }
+            ymax = rmax(m);
+        }
+        const bool use = ok && ymax <= (T)1000;
+        wv.sync();
+        if (t < N) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
+        }
+        stats(false, (T)0, (T)0);
+        theta_max = (T)1e4 * tmax((T)1, theta);
+        theta_min = (T)1e-4 * tmax((T)1, theta);
+        dw_last = 0;
+        acc_alpha = 0;
+        acc_z = 0;
+        iter = 0;
+        nf = 0;
+        kkt = 0;
+    }
+
+    MPCG_HD int begin() {
+        stats(iter > 0, acc_alpha, acc_z);
+        const int nbnd = 2 * (8 * N - 2);
+        const int ng = 6 * N;
+        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
+        const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
+        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
+        const T dual_uns = dual_inf / sf;
+        kkt = tmax(dual_uns, tmax(prim_uns, compl0));
+        int s = 0;
+        if (!isfinite((double)E0))
+            s = IPM_INVALID_NUMBER;
+        else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4)
+            s = IPM_SUCCESS;
+        else if (iter == P.max_iter)
+            s = IPM_MAXITER;
+        s = wv.uni(s);
+        if (s) return s;
+        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
+        const T mu_min = (T)(P.tol / 10.0);
+        for (;;) {
+            const T complmu = tmax(pmax - mu, mu - pmin);
+            const T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+            if (wv.uni(Emu > kappa_eps * mu || mu <= mu_min)) break;
+            const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
+            if (wv.uni(mnew >= mu)) break;
+            mu = mnew;
+            tau = tmax((T)0.99, (T)1 - mu);
+            nf = 0;
+        }
+        wv.mark(7);
+        return 0;
+    }
+
+    MPCG_HD int newton() {
+        T delta_w = 0;
+        int attempt = 0;
+        bool ok = false;
+        for (;;) {
+            if (riccati(0, delta_w)) {
+                ok = true;
+                if (delta_w > 0) dw_last = delta_w;
+                break;
+            }
+            if (attempt == 0)
+                delta_w = (dw_last == 0) ? (T)1e-4 : tmax((T)1e-20, dw_last / (T)3);
+            else
+                delta_w = (dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
+            ++attempt;
+            if (wv.uni(delta_w > (T)1e40)) break;
+        }
+        return ok ? 0 : IPM_ERROR_IN_STEP;
+    }
+
+    MPCG_HD int linesearch(const Fwd& F) {
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
+        const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
+        const T phik = sf * fval - mu * logsum;
+        const T thetak = theta;
+        const T gd = F.gd;
+        const int cap = P.filter_cap;
+        T alpha_min;
+        if (gd < 0 && thetak <= theta_min)
+            alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd,
+                                                             delta_sw * (T)pow((double)thetak, (double)s_theta) /
+                                                                 (T)pow((double)-gd, (double)s_phi)));
+        else if (gd < 0)
+            alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
+        else
+            alpha_min = gamma_alpha * gamma_theta;
+        const bool tiny = F.rel < (T)(10.0 * 2.2e-16);
+        T alpha = F.amax_p;
+        bool accepted = false, ftype = false;
+        const int fi = L.FI();
+        for (int ls = 0; ls < 60; ++ls) {
+            if (wv.uni(tiny)) { accepted = true; ftype = true; break; }
+            if (wv.uni(alpha < alpha_min)) break;
+            T phit, thetat;
+            const bool okt = trial(alpha, &phit, &thetat);
+            if (wv.uni(okt && thetat < theta_max)) {
+                // filter test: lane f checks entry f
+                bool hit = false;
+                for (int f0 = 0; f0 < nf; f0 += 64) {
+                    const int f = f0 + t;
+                    const bool h = f < nf && thetat >= ld(fi + 2 * f) && phit >= ld(fi + 2 * f + 1);
+                    hit = hit || wv.any(h);
+                }
+                if (!hit) {
+                    const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
+                                                 delta_sw * (T)pow((double)thetak, (double)s_theta));
+                    if (wv.uni(thetak <= theta_min && sw)) {
+                        if (wv.uni(phit <= phik + eta_phi * alpha * gd)) { accepted = true; ftype = true; break; }
+                    } else if (wv.uni(thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak)) {
+                        accepted = true;
+                        ftype = false;
+                        break;
+                    }
+                }
+            }
+            alpha *= (T)0.5;
+        }
+        if (!accepted) return IPM_RESTORATION_FAILURE;
+        if (!ftype) {
+            int slot = nf;
+            if (nf == cap) {  // full: drop the oldest entry
+                T e0 = 0, e1 = 0;
+                for (int f0 = 0; f0 < cap; f0 += 64) {
+                    const int f = f0 + t + 1;
+                    wv.sync();
+                    if (f < cap) { e0 = ld(fi + 2 * f); e1 = ld(fi + 2 * f + 1); }
+                    wv.sync();
+                    if (f < cap) { st(fi + 2 * (f - 1), e0); st(fi + 2 * (f - 1) + 1, e1); }
+                }
+                slot = cap - 1;
+            } else {
+                ++nf;
+            }
+            wv.sync();
+            if (t == 0) {
+                st(fi + 2 * slot, ((T)1 - gamma_theta) * thetak);
+                st(fi + 2 * slot + 1, phik - gamma_phi * thetak);
+            }
+        }
+        acc_alpha = alpha;
+        acc_z = F.amax_z;
+        wv.mark(6);
+        return 0;
+    }
+
+    MPCG_HD void solve() {
+        init();
+        for (;;) {
+            int s = begin();
+            if (s) { status = s; break; }
+            s = newton();
+            if (s) { status = s; break; }
+            const Fwd F = forward(0);
+            s = linesearch(F);
+            if (s) { status = s; break; }
+            ++iter;
+        }
+        wv.sync();
+    }
+
+    // Final point with honor_original_bounds projection.
+    MPCG_HD T x_state(int j, int k) const { return tmin(tmax(ld(L.W(k) + j), sl0), su0); }
+    MPCG_HD T x_ctrl(int j, int k) const {
+        const T v = ld(L.W(k) + 6 + j);
+        return j == 0 ? tmin(tmax(v, wl0), wu0) : tmin(tmax(v, al0), au0);
+    }
+    MPCG_HD T objective_out() {
+        T f = 0;
+        if (t < N) {
+            const int k = t;
+            T s[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) s[j] = x_state(j, k);
+            f = cost_state(s);
+            if (k < N - 1) {
+                const T u[2] = {x_ctrl(0, k), x_ctrl(1, k)};
+                T up[2] = {0, 0};
+                if (k <= N - 3) { up[0] = x_ctrl(0, k + 1); up[1] = x_ctrl(1, k + 1); }
+                f += cost_ctrl(k, u, up);
+            }
+        }
+        return rsum(f);
+    }
+};
+
+}  // namespace mpcg
+#endif

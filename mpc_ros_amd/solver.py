@@ -18,13 +18,23 @@ IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor
 
 
 class BatchSolver:
-    def __init__(self, device: int = 0, params: dict | None = None, **ipopt):
+    def __init__(self, device: int = 0, params: dict | None = None, strategy: str = "auto", **ipopt):
         L = _lib.lib()
         h = C.c_void_p()
         _lib.check(L.mpcg_create(int(device), C.byref(h)), "mpcg_create")
         self._h = h
         self.device = device
         self.set_params(params if params is not None else PLUGIN_DEFAULTS, **ipopt)
+        self.set_strategy(strategy)
+
+    def set_strategy(self, strategy: str = "auto"):
+        """'auto' | 'lane' (one problem per lane) | 'wave' (one problem per wavefront, LDS-resident)."""
+        _lib.check(_lib.lib().mpcg_set_strategy(self._h, _lib.STRATEGY[strategy]), "mpcg_set_strategy")
+
+    @property
+    def strategy(self) -> str:
+        v = _lib.lib().mpcg_get_strategy(self._h)
+        return {v2: k for k, v2 in _lib.STRATEGY.items()}[v]
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -1,0 +1,120 @@
+// tests/native/wide_host_check.cpp -- TEST HARNESS ONLY.
+//
+// Runs the one-problem-per-wavefront solver (mpc_ros_amd/csrc/wide_core.h) on the
+// host: the 64 lanes of a wavefront are 64 threads, LDS is a shared array, a lane
+// exchange is a store / barrier / load / barrier, and the wave barrier is a
+// std::barrier.  The butterflies run the same pairwise operations as the device
+// shuffles.  Same stdin/stdout format as ipm_host_check.cpp.  Never part of the
+// product library.
+#include <barrier>
+#include <cmath>
+#include <cstdio>
+#include <thread>
+#include <vector>
+
+#include "../../mpc_ros_amd/csrc/wide_core.h"
+
+struct HostShared {
+    std::barrier<> bar{64};
+    double xd[64];
+    int xi[64];
+    std::vector<double> lds;
+};
+
+struct HostWave {
+    HostShared* sh;
+    int t;
+    double* S;
+    void sync() const { sh->bar.arrive_and_wait(); }
+    double xor_(double v, int m) const {
+        sh->xd[t] = v;
+        sync();
+        const double r = sh->xd[t ^ m];
+        sync();
+        return r;
+    }
+    double up1(double v) const {
+        sh->xd[t] = v;
+        sync();
+        const double r = t > 0 ? sh->xd[t - 1] : v;
+        sync();
+        return r;
+    }
+    bool any(bool b) const {
+        sh->xi[t] = b ? 1 : 0;
+        sync();
+        int r = 0;
+        for (int i = 0; i < 64; ++i) r |= sh->xi[i];
+        sync();
+        return r != 0;
+    }
+    int uni(int v) const { return v; }
+    void mark(int) const {}
+    void ld2(int i, double& a, double& b) const {
+        a = S[i];
+        b = S[i + 1];
+    }
+    double from(double v, int src) const {
+        sh->xd[t] = v;
+        sync();
+        const double r = sh->xd[src];
+        sync();
+        return r;
+    }
+    template <int q>
+    double bcast8(double v) const { return from(v, (t & ~7) | q); }
+    // reduction partners of the device (wave_dev.h): xor 1, xor 2, mirror 8, mirror 16, xor 16, xor 32
+    template <int s>
+    double rpart(double v) const {
+        const int p = s == 0 ? t ^ 1 : s == 1 ? t ^ 2 : s == 2 ? (t & ~7) | (7 - (t & 7))
+                    : s == 3 ? (t & ~15) | (15 - (t & 15)) : s == 4 ? t ^ 16 : t ^ 32;
+        return from(v, p);
+    }
+};
+
+int main() {
+    mpcg::IpmParams P{};
+    if (std::scanf("%d %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %d", &P.N, &P.dt, &P.ref_cte,
+                   &P.ref_eth, &P.ref_v, &P.w_cte, &P.w_eth, &P.w_v, &P.w_w, &P.w_a, &P.w_dw, &P.w_da, &P.max_w,
+                   &P.max_a, &P.bound, &P.tol, &P.max_iter) != 17)
+        return 1;
+    P.bound_relax_factor = 1e-8;
+    P.mu_init = 0.1;
+    P.filter_cap = 64;
+    long B;
+    if (std::scanf("%ld", &B) != 1) return 1;
+    const mpcg::WideLayout L{P.N, P.filter_cap};
+    for (long b = 0; b < B; ++b) {
+        mpcg::IpmProblem<double> pr;
+        for (double& v : pr.init) std::scanf("%lf", &v);
+        for (double& v : pr.c) std::scanf("%lf", &v);
+        HostShared sh;
+        sh.lds.assign(L.total(), std::nan(""));
+        int status = 0, iters = 0;
+        double obj = 0, u0 = 0, u1 = 0;
+        std::vector<double> traj(3 * P.N);
+        std::vector<std::thread> th;
+        for (int t = 0; t < 64; ++t) {
+            th.emplace_back([&, t]() {
+                HostWave wv{&sh, t, sh.lds.data()};
+                mpcg::WideSolver<HostWave> S(P, pr, wv);
+                S.solve();
+                const double o = S.objective_out();
+                if (t == 0) {
+                    status = S.status;
+                    iters = S.iter;
+                    obj = o;
+                    u0 = S.x_ctrl(0, 0);
+                    u1 = S.x_ctrl(1, 0);
+                    for (int s = 0; s < 3; ++s)
+                        for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
+                }
+            });
+        }
+        for (auto& x : th) x.join();
+        std::printf("%d %d %.17g %.17g %.17g", status, iters, obj, u0, u1);
+        for (double v : traj) std::printf(" %.17g", v);
+        std::printf("\n");
+    }
+    return 0;
+}

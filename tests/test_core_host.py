@@ -56,3 +56,33 @@ def test_core_matches_oracle_variants(harness, variants_golden, name):
     g = variants_golden[name]
     r = run_harness(harness, params_from_array(g["params"]), g["state"], g["coeffs"])
     compare(r, g)
+
+
+# ---------------------------------------------------------------- wavefront solver
+# tests/native/wide_host_check.cpp runs mpc_ros_amd/csrc/wide_core.h (one problem per
+# wavefront: stage-parallel sweeps, 64-lane Riccati) with 64 host threads standing in
+# for the lanes.  Summation orders differ from the oracle's (tree reductions), so the
+# comparison is to rounding: same status and iteration count, controls within 1e-9.
+@pytest.fixture(scope="module")
+def wide_harness(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("whc") / "wide_host_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++20", "-w", "-pthread", "-o", exe,
+                           os.path.join(ROOT, "tests", "native", "wide_host_check.cpp")])
+    return exe
+
+
+def test_wide_core_matches_oracle_infinity_subset(wide_harness, infinity_golden):
+    g = infinity_golden
+    sel = np.r_[0:24, 256:264]  # course samples + edge cases
+    sub = {k: g[k][sel] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
+    compare(r, sub, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["class_defaults", "rate_w", "N40", "N3", "small_bound"])
+def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
+    g = variants_golden[name]
+    n = 6
+    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
+    compare(r, sub, atol=1e-9)

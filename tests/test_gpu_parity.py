@@ -18,6 +18,8 @@ from conftest import ROOT, params_from_array
 pytestmark = pytest.mark.gpu
 
 ATOL = 1e-7
+# kernel strategies: one problem per lane (state in HBM) / per wavefront (state in LDS)
+STRATS = ["lane", "wave"]
 
 
 @pytest.fixture(scope="module")
@@ -50,20 +52,31 @@ def test_native_library_is_the_path(torch_cuda):
     assert os.path.samefile(L._name, os.path.join(ROOT, "mpc_ros_amd", "libmpcg.so"))
 
 
-def test_infinity_set_matches_oracle(torch_cuda, infinity_golden):
+def test_auto_strategy(torch_cuda):
+    from mpc_ros_amd import params
+
+    assert solver_for(params.PLUGIN_DEFAULTS).strategy == "wave"
+    assert solver_for(dict(params.PLUGIN_DEFAULTS, STEPS=100)).strategy == "lane"
+    assert solver_for(params.PLUGIN_DEFAULTS, strategy="lane").strategy == "lane"
+
+
+@pytest.mark.parametrize("strategy", STRATS)
+def test_infinity_set_matches_oracle(torch_cuda, infinity_golden, strategy):
     g = infinity_golden
-    r = solver_for(params_from_array(g["params"])).solve(g["state"], g["coeffs"])
+    r = solver_for(params_from_array(g["params"]), strategy=strategy).solve(g["state"], g["coeffs"])
     check_against(r, g)
 
 
+@pytest.mark.parametrize("strategy", STRATS)
 @pytest.mark.parametrize("name", ["class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound"])
-def test_variants_match_oracle(torch_cuda, variants_golden, name):
+def test_variants_match_oracle(torch_cuda, variants_golden, name, strategy):
     g = variants_golden[name]
-    r = solver_for(params_from_array(g["params"])).solve(g["state"], g["coeffs"])
+    r = solver_for(params_from_array(g["params"]), strategy=strategy).solve(g["state"], g["coeffs"])
     check_against(r, g)
 
 
-def test_fresh_problems_against_oracle(torch_cuda, oracle):
+@pytest.mark.parametrize("strategy", STRATS)
+def test_fresh_problems_against_oracle(torch_cuda, oracle, strategy):
     """Problems that are not in the fixtures, solved by both on this box."""
     from mpc_ros_amd import infinity, params
 
@@ -71,7 +84,7 @@ def test_fresh_problems_against_oracle(torch_cuda, oracle):
     st, cf = infinity.make_problems(idx)
     P = params.PLUGIN_DEFAULTS
     ref = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ipm_opts(tol=1e-8), nthreads=16)
-    r = solver_for(P).solve(st, cf)
+    r = solver_for(P, strategy=strategy).solve(st, cf)
     check_against(r, ref)
 
 
@@ -109,10 +122,11 @@ def test_cpp_dropin_class(torch_cuda, tmp_path, infinity_golden):
         assert int(vals[-1]) == g["status"][b]
 
 
+@pytest.mark.parametrize("strategy", STRATS)
 @pytest.mark.parametrize("B", [1, 63, 65, 200])
-def test_ragged_batches(torch_cuda, infinity_golden, B):
+def test_ragged_batches(torch_cuda, infinity_golden, B, strategy):
     g = infinity_golden
-    r = solver_for(params_from_array(g["params"])).solve(g["state"][:B], g["coeffs"][:B])
+    r = solver_for(params_from_array(g["params"]), strategy=strategy).solve(g["state"][:B], g["coeffs"][:B])
     np.testing.assert_allclose(r["u0"], g["u0"][:B], atol=ATOL)
     np.testing.assert_array_equal(r["status"], g["status"][:B])
 
@@ -124,7 +138,8 @@ def test_empty_batch(torch_cuda):
     assert r["u0"].shape == (0, 2)
 
 
-def test_full_size_properties(torch_cuda, oracle):
+@pytest.mark.parametrize("strategy", STRATS)
+def test_full_size_properties(torch_cuda, oracle, strategy):
     """B = 65536 (the benchmark shard): every problem solves; results are deterministic
     and independent of batch position; a random sample agrees with the oracle and
     carries a first-order certificate."""
@@ -134,7 +149,7 @@ def test_full_size_properties(torch_cuda, oracle):
     B = 65536
     P = params.PLUGIN_DEFAULTS
     st, cf = infinity.make_problems(np.arange(B))
-    s = solver_for(P)
+    s = solver_for(P, strategy=strategy)
     dev = torch.device("cuda:0")
     tst, tcf = torch.from_numpy(st).to(dev), torch.from_numpy(cf).to(dev)
     outs = []
@@ -158,3 +173,19 @@ def test_full_size_properties(torch_cuda, oracle):
     np.testing.assert_allclose(u0[sample], ref["u0"], atol=ATOL)
     # controls inside the box (honor_original_bounds)
     assert np.abs(u0[:, 0]).max() <= P["ANGVEL"] and np.abs(u0[:, 1]).max() <= P["MAXTHR"]
+
+
+def test_strategies_agree_at_full_size(torch_cuda):
+    """Both kernel strategies run the same algorithm: same statuses and iteration
+    counts, controls equal to rounding, on the whole benchmark shard."""
+    from mpc_ros_amd import infinity, params
+
+    B = 65536
+    P = params.PLUGIN_DEFAULTS
+    st, cf = infinity.make_problems(np.arange(B))
+    a = solver_for(P, strategy="lane").solve(st, cf)
+    b = solver_for(P, strategy="wave").solve(st, cf)
+    assert np.mean(a["status"] == b["status"]) > 0.999
+    assert np.mean(a["iters"] == b["iters"]) > 0.99
+    same = a["status"] == b["status"]
+    assert np.abs(a["u0"][same] - b["u0"][same]).max() < 1e-6
