@@ -24,7 +24,9 @@ struct WideArgs {
     int32_t* iters;
 };
 
-__global__ void __launch_bounds__(64) k_solve_wide(WideArgs a) {
+// 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
+// budget of 256 per lane lets all of them be resident
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     extern __shared__ double smem[];
     const int64_t p = blockIdx.x;
     if (p >= a.B) return;

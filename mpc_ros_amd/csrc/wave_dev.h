@@ -9,7 +9,7 @@
 //                   within 8, mirror within 16 (DPP row_half_mirror / row_mirror),
 //                   xor 16 (ds_swizzle), xor 32 (ds_bpermute).  Pairs are symmetric, so
 //                   a commutative op leaves every lane with identical bits;
-//   up1(v)          value of lane t-1 (lane 0: its own);
+//   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
 //   any(b), uni(i)  wave vote, wave-uniform (scalar) copy of lane 0's value;
 //   ld2(i, a, b)    16-byte LDS load of two consecutive doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
@@ -67,7 +67,10 @@ struct DevWaveBase {
         if (s == 4) return swz<0x1F | (0x10 << 10)>(v);  // xor 16
         return __shfl_xor(v, 32, 64);
     }
-    __device__ __forceinline__ double up1(double v) const { return __shfl_up(v, 1, 64); }
+    // DPP wave_shr:1 (a gfx9-family DPP control): lane t reads lane t-1
+    __device__ __forceinline__ double up1(double v) const { return dpp<0x138>(v); }
+    // DPP wave_shl:1: lane t reads lane t+1
+    __device__ __forceinline__ double dn1(double v) const { return dpp<0x130>(v); }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
     __device__ __forceinline__ int uni(int v) const { return __builtin_amdgcn_readfirstlane(v); }
 };

@@ -57,15 +57,13 @@ struct WideLayout {
     MPCG_HD int DW(int k) const { return 24 * N + 8 * k; }
     MPCG_HD int Y(int k) const { return 32 * N + 8 * k; }
     MPCG_HD int YP(int k) const { return 40 * N + 8 * k; }
-    MPCG_HD int PM(int k) const { return 48 * N + 36 * k; }  // packed symmetric 8x8 (pidx)
-    MPCG_HD int PV(int k) const { return 84 * N + 8 * k; }
-    MPCG_HD int KR(int k) const { return 92 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
-    MPCG_HD int ST(int k) const { return 108 * N + SS * k; }
-    // scratch of the Riccati sweep: M[64] | Z[16] C0 C1 0
-    MPCG_HD int SCR() const { return 152 * N; }
-    MPCG_HD int RSC() const { return 152 * N + 88; }  // row scales: ra[6] rb[6] 1.0 (+pad)
-    MPCG_HD int FI() const { return 152 * N + 104; }
-    MPCG_HD int total() const { return 152 * N + 104 + 2 * cap; }
+    MPCG_HD int KR(int k) const { return 48 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
+    MPCG_HD int ST(int k) const { return 64 * N + SS * k; }
+    // scratch of the Riccati sweep: M^T (M[r][c] at 8 c + r)
+    MPCG_HD int SCR() const { return 108 * N; }
+    MPCG_HD int RSC() const { return 108 * N + 72; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int FI() const { return 108 * N + 88; }
+    MPCG_HD int total() const { return 108 * N + 88 + 2 * cap; }
 };
 
 template <class WV>
@@ -483,6 +481,9 @@ struct WideSolver {
     // slot of augmented-state column j among the A_hat columns of G (-1: zero column)
     MPCG_HD static int aslot(int j) { return j < 4 ? j : (j == 5 ? 4 : -1); }
 
+    // Riccati sweep.  Lane (i, j) keeps entry (i, j) of the cost-to-go matrix P (and
+    // p_i) in registers; nothing of P is stored: the forward pass needs only the gains,
+    // and the multipliers come from the adjoint recursion (forward()).
     MPCG_HD bool riccati(int mode, T delta_w) {
         wv.sync();
         precompute(mode, delta_w);
@@ -497,9 +498,9 @@ struct WideSolver {
             go[q] = goff(j, q);
             ao[q] = goff(si, q);
         }
-        // M columns sj and si (clamped, masked by hj / hi) and the rate-coupling entries of S_tilde
+        // columns sj and si of M (clamped, masked by hj / hi) and the rate-coupling entries of S_tilde
         const bool hj = sj >= 0, hi = si >= 0;
-        const int mj = sm + (hj ? sj : 0), mi = sm + (hi ? si : 0);
+        const int mj = sm + 8 * (hj ? sj : 0), mi = sm + 8 * (hi ? si : 0);
         const int c0j = j == 6 ? W_::SCC : W_::SZERO, c1j = j == 7 ? W_::SCC + 1 : W_::SZERO;
         const int c0i = i == 6 ? W_::SCC : W_::SZERO, c1i = i == 7 ? W_::SCC + 1 : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
@@ -511,21 +512,19 @@ struct WideSolver {
         q2 = (i == 5 && j == 5) ? W_::SCV + 3 : q2;
         q2 = ((i == 5 && j == 3) || (i == 3 && j == 5)) ? W_::SCV + 4 : q2;
         const int qv = i < 6 ? W_::SQV + i : W_::SZERO;
-        const bool wr = j <= i;  // lane writes the packed record entry
-        const int pw = pidx(i, j);
         wv.sync();
         wv.mark(1);
-        // terminal stage; lane (i, j) keeps P(i, j) in a register from here on
-        T Pij;
+        // terminal stage
+        T Pij, pvi;
         {
             const int sb = L.ST(N - 1);
             Pij = ld(sb + q1);
-            if (wr) st(L.PM(N - 1) + pw, Pij);
-            if (j == 0) st(L.PV(N - 1) + i, ld(sb + qv));
+            pvi = ld(sb + qv);
         }
+        bool bad = false;  // a stage's reduced Hessian not positive definite
         for (int k = N - 2; k >= 0; --k) {
             const int sb = L.ST(k);
-            // row i of P' from the 8 lanes of the row; column j of G from the stage table
+            // row i of P' from the 8 lanes of the row
             T pr_[8], g[8];
             pr_[0] = wv.template bcast8<0>(Pij);
             pr_[1] = wv.template bcast8<1>(Pij);
@@ -537,33 +536,29 @@ struct WideSolver {
             pr_[7] = wv.template bcast8<7>(Pij);
 #pragma unroll
             for (int q = 0; q < 8; ++q) g[q] = ld(sb + go[q]);
-            wv.sync();
             // M = P' G, entry (i, j) per lane; column 7 adds p' (h = P' d + p')
-            T m0 = (j == 7) ? ld(L.PV(k + 1) + i) : (T)0, m1 = 0;
+            T m0 = (j == 7) ? pvi : (T)0, m1 = 0;
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
                 m0 += pr_[q] * g[q];
                 m1 += pr_[q + 1] * g[q + 1];
             }
-            st(sm + t, m0 + m1);
+            wv.sync();  // the previous stage's reads of M are done
+            st(sm + 8 * j + i, m0 + m1);
             wv.sync();
-            // every lane reads the entries of M it needs: columns sj (all rows), 7 (all rows),
-            // the B_hat rows (2,3,5,6,7) of columns 5, 6 and si
+            // columns of M: sj and 7 (all rows), B_hat rows (2,3,5,6,7) of 5, 6 and si
             T mc[8], m7[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                mc[q] = ld(mj + 8 * q);
-                m7[q] = ld(sm + 8 * q + 7);
-            }
-            const T m25 = ld(sm + 21), m55 = ld(sm + 45), m65 = ld(sm + 53);
-            const T m26 = ld(sm + 22), m56 = ld(sm + 46), m66 = ld(sm + 54), m36 = ld(sm + 30), m76 = ld(sm + 62);
-            const T mi2 = ld(mi + 16), mi3 = ld(mi + 24), mi5 = ld(mi + 40), mi6 = ld(mi + 48), mi7 = ld(mi + 56);
-            T qd6, qd7, qv6, qv7;
-            ld2(sb + W_::SQD + 6, qd6, qd7);
-            ld2(sb + W_::SQV + 6, qv6, qv7);
+            ldv<8>(mj, mc);
+            ldv<8>(sm + 56, m7);
+            const T m25 = ld(sm + 42), m55 = ld(sm + 45), m65 = ld(sm + 46);
+            const T m26 = ld(sm + 50), m36 = ld(sm + 51), m56 = ld(sm + 53), m66 = ld(sm + 54), m76 = ld(sm + 55);
+            const T mi2 = ld(mi + 2), mi3 = ld(mi + 3), mi5 = ld(mi + 5), mi6 = ld(mi + 6), mi7 = ld(mi + 7);
             T c[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) c[q] = ld(sb + ao[q]);
+            T qd6, qd7, qv6, qv7;
+            ld2(sb + W_::SQD + 6, qd6, qd7);
+            ld2(sb + W_::SQV + 6, qv6, qv7);
             const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
             const T qh = ld(sb + q1) + ld(sb + q2);
             const T qvi = ld(sb + qv);
@@ -572,10 +567,7 @@ struct WideSolver {
             const T Rt01 = dt * (m26 + m56) + m66;
             const T Rt11 = qd7 + (dt * m36 + m76);
             const T det = Rt00 * Rt11 - Rt01 * Rt01;
-            if (wv.uni(!(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11))) {
-                wv.mark(2);
-                return false;
-            }
+            bad = bad || !(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11);
             const T rt0 = qv6 + (dt * (m7[2] + m7[5]) + m7[6]);
             const T rt1 = qv7 + (dt * m7[3] + m7[7]);
             const T rdet = rcp(det);
@@ -598,8 +590,7 @@ struct WideSolver {
                 h1 += c[q + 1] * m7[q + 1];
             }
             Pij = qh + (hj ? a0 + a1 : (T)0) + s0i * K0 + s1i * K1;
-            if (wr) st(L.PM(k) + pw, Pij);
-            if (j == 0) st(L.PV(k) + i, qvi + (h0 + h1) + s0i * kf0 + s1i * kf1);
+            pvi = qvi + (h0 + h1) + s0i * kf0 + s1i * kf1;
             if (i == 0) {
                 st(L.KR(k) + j, K0);
                 st(L.KR(k) + 8 + j, K1);
@@ -608,6 +599,11 @@ struct WideSolver {
                 st(sb + W_::SKF, kf0);
                 st(sb + W_::SKF + 1, kf1);
             }
+        }
+        // a failed inertia test anywhere (the stages after it computed values the retry overwrites)
+        if (wv.uni(bad)) {
+            wv.mark(2);
+            return false;
         }
         wv.mark(2);
         return true;
@@ -632,94 +628,137 @@ struct WideSolver {
 
     MPCG_HD Fwd forward(int mode) {
         wv.sync();
-        // the step recursion, replicated in every lane; stage k+1's records are read
-        // while stage k computes
-        T ds[8];
+        // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
+        // systolically: lane k holds stage k's records, every step every lane applies its
+        // own stage map to the vector it holds and passes the result one lane up, so lane
+        // k sees its correct input at step k (and keeps it).
+        T K[16], kf[2], a[8], d[6];
+        if (t < N - 1) {
+            ldv<16>(L.KR(t), K);
+            ldv<2>(L.ST(t) + WideLayout::SKF, kf);
+            ldv<8>(L.ST(t) + WideLayout::SA, a);
+            ldv<6>(L.ST(t) + WideLayout::SD, d);
+        } else {  // last stage (and idle lanes): no control, du = 0
+#pragma unroll
+            for (int q = 0; q < 16; ++q) K[q] = 0;
+            kf[0] = 0;
+            kf[1] = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = 0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) d[q] = 0;
+        }
+        T x[8], xk[8], duk[2];
         {
             T w0[6];
             ldn<6>(L.W(0), w0);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) ds[j] = (mode == 0) ? -(w0[j] - pr.init[j]) : (T)0;
-            ds[6] = 0;
-            ds[7] = 0;
+            for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && t == 0) ? -(w0[j] - pr.init[j]) : (T)0;
+            x[6] = 0;
+            x[7] = 0;
         }
-        T K[16], kf[2], a[8], d[6];
-        ldv<16>(L.KR(0), K);
-        ldv<2>(L.ST(0) + WideLayout::SKF, kf);
-        ldv<8>(L.ST(0) + WideLayout::SA, a);
-        ldv<6>(L.ST(0) + WideLayout::SD, d);
-        for (int k = 0; k < N - 1; ++k) {
-            T Kn[16], kfn[2], an[8], dn[6];
-            const int kn = k + 1 < N - 1 ? k + 1 : k;
-            ldv<16>(L.KR(kn), Kn);
-            ldv<2>(L.ST(kn) + WideLayout::SKF, kfn);
-            ldv<8>(L.ST(kn) + WideLayout::SA, an);
-            ldv<6>(L.ST(kn) + WideLayout::SD, dn);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xk[q] = 0;
+        duk[0] = 0;
+        duk[1] = 0;
+        for (int s = 0; s < N; ++s) {
             T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
 #pragma unroll
             for (int m = 0; m < 8; m += 2) {
-                u0a += K[m] * ds[m];
-                u0b += K[m + 1] * ds[m + 1];
-                u1a += K[8 + m] * ds[m];
-                u1b += K[9 + m] * ds[m + 1];
+                u0a += K[m] * x[m];
+                u0b += K[m + 1] * x[m + 1];
+                u1a += K[8 + m] * x[m];
+                u1b += K[9 + m] * x[m + 1];
             }
             const T du0 = u0a + u0b, du1 = u1a + u1b;
-            if (t == 0) {
+            if (t == s) {
 #pragma unroll
-                for (int j = 0; j < 6; ++j) st(L.DW(k) + j, ds[j]);
-                st(L.DW(k) + 6, du0);
-                st(L.DW(k) + 7, du1);
+                for (int q = 0; q < 8; ++q) xk[q] = x[q];
+                duk[0] = du0;
+                duk[1] = du1;
             }
-            T nx6[6];
-            A_mul(a, ds, nx6);
-            nx6[2] += dt * du0;
-            nx6[3] += dt * du1;
-            nx6[5] += dt * du0;
+            T y[8];
+            A_mul(a, x, y);
+            y[2] += dt * du0;
+            y[3] += dt * du1;
+            y[5] += dt * du0;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) ds[j] = nx6[j] + d[j];
-            ds[6] = du0;
-            ds[7] = du1;
+            for (int j = 0; j < 6; ++j) y[j] += d[j];
+            y[6] = du0;
+            y[7] = du1;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) K[q] = Kn[q];
-            kf[0] = kfn[0];
-            kf[1] = kfn[1];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] = an[q];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) d[q] = dn[q];
+            for (int q = 0; q < 8; ++q) x[q] = wv.up1(y[q]);
         }
-        if (t == 0) {
+        if (t < N) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) st(L.DW(N - 1) + j, ds[j]);
-            st(L.DW(N - 1) + 6, 0);
-            st(L.DW(N - 1) + 7, 0);
+            for (int j = 0; j < 6; j += 2) {
+                // 16-byte stores of the step of stage t
+                st(L.DW(t) + j, xk[j]);
+                st(L.DW(t) + j + 1, xk[j + 1]);
+            }
+            st(L.DW(t) + 6, duk[0]);
+            st(L.DW(t) + 7, duk[1]);
         }
-        wv.sync();
+        // Multipliers of the dynamics rows into stage k from stationarity in s_k:
+        //   lam_k = Q_k ds_k + q_k + A_k^T lam_{k+1},   yh+_k = -lam_k
+        // (rows 0..5 of the Riccati costate P_k ds_k + p_k), a backward systolic pass:
+        // lane k holds stage k's Hessian diagonal and curvature, gradient and A_k.
         wv.mark(3);
+        T lam[6], lk[6], base[6], ak[8];
+        {
+            T qd[8], qv[8], cv[6];
+            if (t < N) {
+                const int sb = L.ST(t);
+                ldv<8>(sb + WideLayout::SQD, qd);
+                ldv<8>(sb + WideLayout::SQV, qv);
+                ldv<6>(sb + WideLayout::SCV, cv);  // cv[0..4] = Q00 Q22 Q32 Q55 Q53
+                ldv<8>(sb + WideLayout::SA, ak);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) { qd[q] = 0; qv[q] = 0; ak[q] = 0; }
+#pragma unroll
+                for (int q = 0; q < 6; ++q) cv[q] = 0;
+            }
+            const T* x = xk;
+            base[0] = (qd[0] + cv[0]) * x[0] + qv[0];
+            base[1] = qd[1] * x[1] + qv[1];
+            base[2] = (qd[2] + cv[1]) * x[2] + cv[2] * x[3] + qv[2];
+            base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
+            base[4] = qd[4] * x[4] + qv[4];
+            base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) { lam[q] = 0; lk[q] = 0; }
+        for (int s = N - 1; s >= 0; --s) {
+            T o[6];
+            AT_mul(ak, lam, o);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) o[q] += base[q];
+            if (t == s) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) lk[q] = o[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lam[q] = wv.dn1(o[q]);
+        }
+        if (t < N) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) st(L.YP(t) + q, -lk[q]);
+        }
+        wv.mark(4);
         Fwd F{(T)1, (T)1, (T)0, (T)0};
         if (t < N) {
             const int k = t;
             const bool last = k == N - 1;
-            T dsk[8];
-            ldn<6>(L.DW(k), dsk);
-            dsk[6] = k >= 1 ? ld(L.DW(k - 1) + 6) : (T)0;
-            dsk[7] = k >= 1 ? ld(L.DW(k - 1) + 7) : (T)0;
-#pragma unroll
-            for (int r = 0; r < 6; ++r) {
-                T acc0 = ld(L.PV(k) + r), acc1 = 0;
-#pragma unroll
-                for (int m = 0; m < 8; m += 2) {
-                    acc0 += ld(L.PM(k) + pidx(r, m)) * dsk[m];
-                    acc1 += ld(L.PM(k) + pidx(r, m + 1)) * dsk[m + 1];
-                }
-                st(L.YP(k) + r, -(acc0 + acc1));
-            }
             if (mode == 0) {
                 T w[8], zl[8], zu[8], dk[8];
                 ldn<8>(L.W(k), w);
                 ldn<8>(L.ZL(k), zl);
                 ldn<8>(L.ZU(k), zu);
-                ldn<8>(L.DW(k), dk);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) dk[q] = xk[q];
+                dk[6] = duk[0];
+                dk[7] = duk[1];
                 T g[6], gu[2] = {0, 0};
                 grad_state(w, g);
                 if (!last) {
@@ -752,7 +791,7 @@ struct WideSolver {
             F.gd = v[2];
             F.rel = v[3];
         }
-        wv.mark(4);
+        wv.mark(5);
         return F;
     }
 
@@ -809,7 +848,7 @@ struct WideSolver {
         thv = v[1];
         lg = v[2];
         const bool anybad = wv.any(bad != 0);
-        wv.mark(5);
+        wv.mark(6);
         *phi = sf * f - mu * lg;
         *th = thv;
         return !anybad && isfinite((double)*phi);
@@ -882,7 +921,7 @@ struct WideSolver {
             tau = tmax((T)0.99, (T)1 - mu);
             nf = 0;
         }
-        wv.mark(7);
+        wv.mark(8);
         return 0;
     }
 
@@ -977,7 +1016,7 @@ struct WideSolver {
         }
         acc_alpha = alpha;
         acc_z = F.amax_z;
-        wv.mark(6);
+        wv.mark(7);
         return 0;
     }
 

@@ -17,8 +17,8 @@
 #include "../mpc_ros_amd/csrc/wide_core.h"
 
 namespace mpcg {
-constexpr int NPH = 8;
-const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-par", "trial", "ls-rest", "begin-rest"};
+constexpr int NPH = 9;
+const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest"};
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
