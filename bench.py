@@ -10,11 +10,15 @@ statuses are gathered to rank 0 (RCCL all-gather over xGMI) -- the only
 collective.  Inputs are resident in HBM before the timed region (weak scaling: the
 per-GPU batch is fixed).  Rank 0 prints one JSON line.
 
-roofline: the dominant (only) kernel, ipm_solve_kernel.  achieved = algorithmic
-bytes per launch (B x 8 x (6 + 4 + 2 + 3N) = B x 576 B at N = 20)
-divided by the kernel's average duration measured with HIP events on the stream
-it runs on; traffic = HBM bytes per launch from the committed rocprofv3 PMC
-summary for this configuration (profiles/), or null.
+roofline: the dominant (only) kernel, mpcg::k_solve_wide (one problem per
+wavefront, whole problem state in LDS).  achieved = algorithmic bytes per launch
+(B x 8 x (6 + 4 + 2 + 3N) = B x 576 B at N = 20) divided by the
+kernel's average duration measured with HIP events on the stream it runs on;
+traffic = memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the committed
+rocprofv3 PMC summary for this configuration (profiles/pmc_B<B>_N<N>.json), or null.
+The path is not HBM-bound: the kernel is FP64-VALU issue/latency
+bound, so the line also carries valu_fp64 = FP64 FLOP/s (PMC-counted FLOPs per
+solve x solves / kernel time) against the 78.6 TFLOP/s vector peak.
 cpu_baseline: the oracle (dense Ipopt restatement, "port") on a bounded sample of
 the same problems, rank 0, N = 1 only.
 """
@@ -74,13 +78,12 @@ def cpu_baseline(P, st, cf, budget_s):
                 iters_mean=float(np.mean(r["iters"])))
 
 
-def pmc_traffic(name):
+def pmc_profile(name):
     path = os.path.join(ROOT, "profiles", f"{name}.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+        return json.load(f)
 
 
 def main():
@@ -156,7 +159,15 @@ def main():
         bytes_per_solve = 8 * (6 + 4 + 2 + 3 * N)
         achieved = count * bytes_per_solve / (kern * 1e-3) / 1e9
         prof = a.profile_name or f"pmc_B{B}_N{N}"
-        traffic = pmc_traffic(prof)
+        pmc = pmc_profile(prof) if solver.strategy == "wave" else {}
+        traffic = pmc.get("hbm_bytes_per_launch")
+        fl = pmc.get("fp64_flops_per_solve")
+        valu = None
+        if fl:
+            got = fl * count / (kern * 1e-3) / 1e12
+            valu = {"achieved": got, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": got / FP64_VALU_PEAK_TFLOPS, "flops_per_solve": fl,
+                    "source": f"profiles/{prof}.json (SQ_INSTS_VALU_FLOPS_FP64)"}
         line = {
             "metric": "NMPC solves/sec (whole node), N=20 diff-drive, at 1/2/4/8 MI355X",
             "value": value,
@@ -175,8 +186,11 @@ def main():
                        "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ipm_solve_kernel", "kernel_ms": kern,
-                         "algorithmic_bytes_per_solve": bytes_per_solve},
+                         "kernel": "mpcg::k_solve_wide" if solver.strategy == "wave" else "lane kernels",
+                         "strategy": solver.strategy, "kernel_ms": kern,
+                         "algorithmic_bytes_per_solve": bytes_per_solve,
+                         "traffic_source": f"profiles/{prof}.json" if traffic else None,
+                         "valu_fp64": valu},
             "solver": {"iters_mean": float(it.mean()), "iters_max": int(it.max()),
                        "success_frac": float(np.mean(sts == 1))},
         }

@@ -27,7 +27,6 @@ struct WideArgs {
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
 // budget of 256 per lane lets all of them be resident
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
-    extern __shared__ double smem[];
     const int64_t p = blockIdx.x;
     if (p >= a.B) return;
     const int t = threadIdx.x;
@@ -36,7 +35,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int j = 0; j < 6; ++j) pr.init[j] = a.state[p * 6 + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) pr.c[j] = a.coeffs[p * 4 + j];
-    DevWave wv{t, (DevWave::ldsT*)smem};
+    DevWave wv;
+    wv.t = t;
     WideSolver<DevWave> S(a.P, pr, wv);
     S.solve();
     const double o = S.objective_out();

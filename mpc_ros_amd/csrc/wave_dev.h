@@ -11,7 +11,7 @@
 //                   a commutative op leaves every lane with identical bits;
 //   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
 //   any(b), uni(i)  wave vote, wave-uniform (scalar) copy of lane 0's value;
-//   ld2(i, a, b)    16-byte LDS load of two consecutive doubles (i even).
+//   S()             the LDS base; ld2(i, a, b): 16-byte LDS load of two doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
 #define MPCG_WAVE_DEV_H
 
@@ -25,11 +25,16 @@ namespace mpcg {
 #define MPCG_LDS
 #endif
 
+// The workgroup's dynamic LDS (one problem per workgroup).  Addressing it through the
+// symbol (a link-time constant) rather than a pointer value lets every LDS access
+// fold its offset into the instruction.
+extern __shared__ double mpcg_dyn_lds[];
+
 struct DevWaveBase {
     typedef MPCG_LDS double ldsT;
     typedef MPCG_LDS double2 ldsT2;
     int t;
-    ldsT* S;
+    __device__ __forceinline__ static ldsT* S() { return (ldsT*)mpcg_dyn_lds; }
 
     __device__ __forceinline__ void sync() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -37,7 +42,7 @@ struct DevWaveBase {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     __device__ __forceinline__ void ld2(int i, double& a, double& b) const {
-        const double2 v = *(const ldsT2*)(S + i);
+        const double2 v = *(const ldsT2*)(S() + i);
         a = v.x;
         b = v.y;
     }

@@ -88,12 +88,12 @@ struct WideSolver {
         : P(P_), pr(pr_), wv(wv_), L{P_.N, P_.filter_cap}, N(P_.N), t(wv_.t), dt((T)P_.dt) {}
 
     // ------------------------------------------------------------ LDS helpers
-    MPCG_HD T ld(int i) const { return wv.S[i]; }
-    MPCG_HD void st(int i, T v) const { wv.S[i] = v; }
+    MPCG_HD T ld(int i) const { return wv.S()[i]; }
+    MPCG_HD void st(int i, T v) const { wv.S()[i] = v; }
     template <int n>
     MPCG_HD void ldn(int i, T* v) const {
 #pragma unroll
-        for (int j = 0; j < n; ++j) v[j] = wv.S[i + j];
+        for (int j = 0; j < n; ++j) v[j] = wv.S()[i + j];
     }
 
     // ------------------------------------------------------ wave reductions

@@ -24,7 +24,8 @@ struct HostShared {
 struct HostWave {
     HostShared* sh;
     int t;
-    double* S;
+    double* lds;
+    double* S() const { return lds; }
     void sync() const { sh->bar.arrive_and_wait(); }
     double xor_(double v, int m) const {
         sh->xd[t] = v;
@@ -51,8 +52,8 @@ struct HostWave {
     int uni(int v) const { return v; }
     void mark(int) const {}
     void ld2(int i, double& a, double& b) const {
-        a = S[i];
-        b = S[i + 1];
+        a = lds[i];
+        b = lds[i + 1];
     }
     double from(double v, int src) const {
         sh->xd[t] = v;

@@ -1,0 +1,76 @@
+"""Summarise rocprofv3 PMC passes (tools/gpu_pmc.sh) of the benchmark kernel into
+profiles/<name>.json, which bench.py reads for roofline.traffic and the FP64-VALU
+figures.
+
+    python tools/pmc_summary.py gpurun_out/pmc profiles/pmc_B65536_N20.json --batch 65536
+
+Counters are per dispatch of mpcg::k_solve_wide (one solve of the whole batch).
+FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters over the L2's
+memory-side requests; MI355X_MICROARCH.md §HBM: Infinity-Cache hits are counted,
+FETCH_SIZE is calibrated only for 16-B-per-lane streaming reads -- this kernel's
+global reads are the 80-B-per-problem inputs and scratch (spill) traffic, so the
+figure is reported raw).  SQ_WAVE_CYCLES / SQ_ACTIVE_INST_ANY / SQ_WAIT_* count
+quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def load(root: str, kernel: str = "k_solve_wide"):
+    vals = collections.defaultdict(list)
+    times = []
+    for f in sorted(glob.glob(os.path.join(root, "*", "*", "*_counter_collection.csv"))):
+        per = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if kernel not in r.get("Kernel_Name", ""):
+                continue
+            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+            times.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+        for (d, c), v in per.items():
+            vals[c].append(v)
+    return {c: sum(v) / len(v) for c, v in vals.items()}, (sum(times) / len(times) if times else None)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("out")
+    ap.add_argument("--batch", type=int, default=65536)
+    a = ap.parse_args()
+    c, t = load(a.root)
+    B = a.batch
+    out = {"kernel": "mpcg::k_solve_wide", "batch": B, "counters_per_dispatch": c, "dispatch_s": t}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["fetch_bytes"] = c["FETCH_SIZE"] * 1024
+        out["write_bytes"] = c["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = out["fetch_bytes"] + out["write_bytes"]
+    if "SQ_WAVES" in c:
+        w = c["SQ_WAVES"]
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+            if k in c:
+                out[k.lower() + "_per_solve"] = c[k] / w
+        if "SQ_WAVE_CYCLES" in c:
+            wc = c["SQ_WAVE_CYCLES"]
+            out["wave_cycles_per_solve"] = 4 * wc / w
+            for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+                if k in c:
+                    out[k.lower() + "_frac"] = c[k] / wc
+    if "GRBM_GUI_ACTIVE" in c and t:
+        out["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
+    if "SQ_INSTS_VALU_FLOPS_FP64" in c:
+        out["fp64_flops_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"] + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
+        out["fp64_flops_per_solve"] = out["fp64_flops_per_launch"] / B
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -35,7 +35,6 @@ struct ProfWave : DevWaveBase {
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_prof(IpmParams P, int64_t B, const double* state, const double* coeffs,
                                              unsigned long long* acc, int* iters, int* status) {
-    extern __shared__ double smem[];
     const int64_t p = blockIdx.x;
     if (p >= B) return;
     IpmProblem<double> pr;
@@ -43,7 +42,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     for (int j = 0; j < 4; ++j) pr.c[j] = coeffs[p * 4 + j];
     ProfWave wv;
     wv.t = (int)threadIdx.x;
-    wv.S = (ProfWave::ldsT*)smem;
     wv.acc = acc + p * (NPH + 1);
     wv.last = (unsigned long long)clock64();
     const unsigned long long t0 = wv.last;
