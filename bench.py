@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--profile-name", default=None, help="PMC summary to read traffic from")
     ap.add_argument("--strategy", default="auto", choices=["auto", "lane", "wave"],
                     help="kernel strategy: one problem per lane / per wavefront")
+    ap.add_argument("--mode", default="solve", choices=["solve", "track"],
+                    help="solve: MPC::Solve on preprocessed inputs (the metric); track: the whole control "
+                         "tick from raw poses and waypoint plans (findBestPath + solve + post-processing)")
     return ap.parse_args()
 
 
@@ -110,6 +113,13 @@ def main():
     st, cf = infinity.make_problems(np.arange(start, start + count))
     tst = torch.from_numpy(st).to(dev)
     tcf = torch.from_numpy(cf).to(dev)
+    if a.mode == "track":
+        sc = infinity.draw_scenarios(np.arange(start, start + count))
+        px, py, yaw, plan = infinity.scenario_poses(sc)
+        tpose = torch.from_numpy(np.ascontiguousarray(np.stack([px, py, yaw], 1))).to(dev)
+        tvel = torch.from_numpy(np.ascontiguousarray(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))).to(dev)
+        tplan = torch.from_numpy(np.ascontiguousarray(plan)).to(dev)
+        cmd = torch.empty((count, 3), dtype=torch.float64, device=dev)
     solver = BatchSolver(dev.index, P, strategy=a.strategy)
     solver.reserve(count)
     u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
@@ -123,12 +133,15 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        solver.solve_device(tst, tcf, u0, traj, status, None, iters, stream=stream)
+        if a.mode == "track":
+            solver.track_device(tpose, tvel, tplan, cmd, traj, status, stream=stream)
+        else:
+            solver.solve_device(tst, tcf, u0, traj, status, None, iters, stream=stream)
         if timed:
             e1.record(stream)
             k_ms.append((e0, e1))
         if world > 1:
-            g_u0 = D.gather_rows(u0, total)
+            g_u0 = D.gather_rows(cmd if a.mode == "track" else u0, total)
             g_st = D.gather_rows(status, total)
             if a.gather_traj:
                 D.gather_rows(traj.view(count, -1), total)
@@ -152,6 +165,9 @@ def main():
         t = torch.tensor([elapsed, kern], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern = float(t[0]), float(t[1])
+    if a.mode == "track":  # iteration counts of the same problems
+        solver.solve_device(tst, tcf, u0, None, None, None, iters, stream=stream)
+        torch.cuda.synchronize()
     it = iters.cpu().numpy()
     sts = status.cpu().numpy()
     if rank == 0:
@@ -183,7 +199,8 @@ def main():
             "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem)",
             "config": {"workload": f"diff-drive NMPC (MPC::Solve NLP, Ipopt algorithm), N={N}, fp64, "
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
-                       "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}"},
+                       "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}",
+                       "mode": a.mode},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mpcg::k_solve_wide" if solver.strategy == "wave" else "lane kernels",

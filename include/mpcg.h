@@ -109,13 +109,28 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
 
-/* Fused pre-processing + solve: Tracking::findBestPath (driving_state.cpp:175-256)
- * on device for B robots, then the solve.  pose [B][3] (x, y, yaw), vel [B][3]
- * (v feedback, previous w, previous throttle), plan [B][M][2] waypoints.
- * Writes state/coeffs (optional, may be NULL) and the solve outputs. */
+/* Tracking::findBestPath's preprocessing (mpc_ros/src/driving_state.cpp:175-256) on the
+ * device for B robots: waypoints to the vehicle frame, cubic polyfit (Householder QR),
+ * cte, heading error from the first int(0.3 M) waypoint increments, delay-mode
+ * prediction.  M waypoints per robot, the same for the batch: 4 <= M <= 64 (polyfit asserts
+ * order 3 <= M - 1, driving_state.cpp:286).
+ *   pose [B][3]  x, y, yaw                       (global_pose)
+ *   vel  [B][3]  v feedback, previous w, previous throttle (feedback_vel.linear.x, _w, _throttle)
+ *   plan [B][M][2] waypoints x, y                (ref_plan)
+ *   state [B][6], coeffs [B][4]                  the arguments of MPC::Solve (outputs)
+ * dt = the handle's DT.  Queued on `stream`; no solve. */
 int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
                            const double* d_plan, int32_t delay_mode, double* d_state, double* d_coeffs,
                            void* stream);
+
+/* One control tick of Tracking::findBestPath for B robots: preprocessing, the solve,
+ * and the post-processing of driving_state.cpp:262-269.
+ *   cmd [B][3]  speed = min(v + throttle dt, REF_V), w = w0, throttle = a0
+ *   traj [B][3][N], status [B]: as mpcg_solve_device (may be NULL).
+ * Intermediate state/coeffs/controls live in handle-owned device buffers. */
+int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
+                      const double* d_plan, int32_t delay_mode, double* d_cmd, double* d_traj, int32_t* d_status,
+                      void* stream);
 
 /* Kernel strategy of the handle's solves (performance only: every strategy runs the
  * same algorithm, results agree to rounding):

@@ -53,6 +53,8 @@ SIGNATURES = {
                            C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_preprocess_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                 C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    "mpcg_track_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_synchronize": ([C.c_void_p], C.c_int),
     "mpcg_set_strategy": ([C.c_void_p, C.c_int32], C.c_int),
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),

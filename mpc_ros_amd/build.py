@@ -12,8 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmpcg.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_kernels.hip", "mpcg_wide.hip", "mpcg_api.cpp", "mpc_planner.cpp")]
-HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "mpcg_internal.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_kernels.hip", "mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpc_planner.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h")] + [
     os.path.join(ROOT, "include", f) for f in ("mpcg.h", "mpc_planner.h")]
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 

@@ -36,6 +36,9 @@ struct mpcg_handle {
     size_t io_bytes = 0;
     mpcg::DriverCtx drv;  // device active counter, pinned readback slots, events
     int strategy = MPCG_STRATEGY_AUTO;
+    // mpcg_track_device intermediates: state [B][6] | coeffs [B][4] | u0 [B][2]
+    double* d_trk = nullptr;
+    size_t trk_bytes = 0;
 };
 
 extern "C" {
@@ -205,6 +208,7 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->ws) hipFree(h->ws);
     if (h->d_io) hipFree(h->d_io);
+    if (h->d_trk) hipFree(h->d_trk);
     if (h->drv.d_active) hipFree(h->drv.d_active);
     if (h->drv.h_active) hipHostFree(h->drv.h_active);
     for (hipEvent_t ev : h->drv.ev)
@@ -352,10 +356,52 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
 int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
                            const double* d_plan, int32_t delay_mode, double* d_state, double* d_coeffs,
                            void* stream) {
-    (void)B; (void)M; (void)d_pose; (void)d_vel; (void)d_plan; (void)delay_mode; (void)d_state; (void)d_coeffs;
-    (void)stream;
     if (!h) return fail(-1, "null handle");
-    return fail(-4, "mpcg_preprocess_device: not built in this version");
+    if (B < 0) return fail(-1, "negative batch");
+    if (B == 0) return 0;
+    // findBestPath returns without solving for an empty plan (driving_state.cpp:182-185);
+    // polyfit asserts order 3 <= M - 1 (:286)
+    if (M < 4 || M > 64) return fail(-1, "M (waypoints per robot) must be in [4, 64]");
+    if (!d_pose || !d_vel || !d_plan || !d_state || !d_coeffs) return fail(-1, "null buffer");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    e = mpcg::launch_find_best_path(B, M, h->params.dt, delay_mode ? 1 : 0, d_pose, d_vel, d_plan, d_state,
+                                    d_coeffs, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "find_best_path launch");
+    return 0;
+}
+
+int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,
+                      const double* d_plan, int32_t delay_mode, double* d_cmd, double* d_traj, int32_t* d_status,
+                      void* stream) {
+    if (!h) return fail(-1, "null handle");
+    if (B < 0) return fail(-1, "negative batch");
+    if (B == 0) return 0;
+    if (!d_cmd) return fail(-1, "cmd is required");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    const size_t need = sizeof(double) * 12 * (size_t)B;
+    if (need > h->trk_bytes) {
+        if (h->d_trk) {
+            hipDeviceSynchronize();  // the old buffers may be in use on any stream
+            hipFree(h->d_trk);
+            h->d_trk = nullptr;
+            h->trk_bytes = 0;
+        }
+        e = hipMalloc((void**)&h->d_trk, need);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(track buffers)");
+        h->trk_bytes = need;
+    }
+    double* st = h->d_trk;
+    double* cf = st + 6 * B;
+    double* u0 = cf + 4 * B;
+    int rc = mpcg_preprocess_device(h, B, M, d_pose, d_vel, d_plan, delay_mode, st, cf, stream);
+    if (rc) return rc;
+    rc = mpcg_solve_device(h, B, st, cf, u0, d_traj, d_status, nullptr, nullptr, stream);
+    if (rc) return rc;
+    e = mpcg::launch_post(B, h->params.dt, h->params.ref_v, d_vel, u0, d_cmd, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "post-processing launch");
+    return 0;
 }
 
 int mpcg_synchronize(mpcg_handle* h) {

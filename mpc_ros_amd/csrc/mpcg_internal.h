@@ -29,5 +29,11 @@ size_t wide_lds_bytes(const IpmParams& P);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, hipStream_t stream);
 
+// findBestPath preprocessing and post-processing (mpcg_track.hip).
+hipError_t launch_find_best_path(int64_t B, int M, double dt, int delay_mode, const double* pose, const double* vel,
+                                 const double* plan, double* state, double* coeffs, hipStream_t stream);
+hipError_t launch_post(int64_t B, double dt, double ref_v, const double* vel, const double* u0, double* cmd,
+                       hipStream_t stream);
+
 }  // namespace mpcg
 #endif

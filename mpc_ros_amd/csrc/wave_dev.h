@@ -10,7 +10,7 @@
 //                   xor 16 (ds_swizzle), xor 32 (ds_bpermute).  Pairs are symmetric, so
 //                   a commutative op leaves every lane with identical bits;
 //   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
-//   any(b), uni(i)  wave vote, wave-uniform (scalar) copy of lane 0's value;
+//   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
 //   S()             the LDS base; ld2(i, a, b): 16-byte LDS load of two doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
 #define MPCG_WAVE_DEV_H
@@ -78,6 +78,10 @@ struct DevWaveBase {
     __device__ __forceinline__ double dn1(double v) const { return dpp<0x130>(v); }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
     __device__ __forceinline__ int uni(int v) const { return __builtin_amdgcn_readfirstlane(v); }
+    __device__ __forceinline__ double uni_d(double v) const {
+        return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                                __builtin_amdgcn_readfirstlane(__double2loint(v)));
+    }
 };
 
 struct DevWave : DevWaveBase {

@@ -59,11 +59,11 @@ struct WideLayout {
     MPCG_HD int YP(int k) const { return 40 * N + 8 * k; }
     MPCG_HD int KR(int k) const { return 48 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
     MPCG_HD int ST(int k) const { return 64 * N + SS * k; }
-    // scratch of the Riccati sweep: M^T (M[r][c] at 8 c + r)
+    // scratch of the Riccati sweep: M^T (M[r][c] at 8 c + r), then P row-major
     MPCG_HD int SCR() const { return 108 * N; }
-    MPCG_HD int RSC() const { return 108 * N + 72; }  // row scales: ra[6] rb[6] 1.0 (+pad)
-    MPCG_HD int FI() const { return 108 * N + 88; }
-    MPCG_HD int total() const { return 108 * N + 88 + 2 * cap; }
+    MPCG_HD int RSC() const { return 108 * N + 128; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int FI() const { return 108 * N + 144; }
+    MPCG_HD int total() const { return 108 * N + 144 + 2 * cap; }
 };
 
 template <class WV>
@@ -109,6 +109,8 @@ struct WideSolver {
         for (int q = 0; q < n; ++q)
             v[q] = op[q] == RSUM ? v[q] + o[q] : (op[q] == RMAX ? tmax(v[q], o[q]) : tmin(v[q], o[q]));
     }
+    // Contributions come from lanes < N only: for N <= 32 five steps complete the
+    // reduction in lanes 0..31 and lane 0's value is made wave-uniform (scalar).
     template <int n>
     MPCG_HD void reduce(T* v, const int* op) {
         rstep<0, n>(v, op);
@@ -116,7 +118,9 @@ struct WideSolver {
         rstep<2, n>(v, op);
         rstep<3, n>(v, op);
         rstep<4, n>(v, op);
-        rstep<5, n>(v, op);
+        if (N > 32) rstep<5, n>(v, op);
+#pragma unroll
+        for (int q = 0; q < n; ++q) v[q] = wv.uni_d(v[q]);
     }
     MPCG_HD T rsum(T v) {
         const int op[1] = {RSUM};
@@ -211,7 +215,7 @@ struct WideSolver {
             grad_state(z, g);
             gm = tmax(gm, tmax((T)fabs(g[3]), tmax((T)fabs(g[4]), (T)fabs(g[5]))));
         }
-        sf = gm > (T)100 ? (T)100 / gm : (T)1;
+        sf = wv.uni_d(gm > (T)100 ? (T)100 / gm : (T)1);
         T ra[6], rb[6];
         rowscales_at(pr.init, ra);
         const T z6[6] = {0, 0, 0, 0, 0, 0};
@@ -296,6 +300,10 @@ struct WideSolver {
             ldn<8>(L.ZL(k), zl);
             ldn<8>(L.ZU(k), zu);
             ldn<6>(L.Y(k), y);
+            // linearisation at the iterate, kept in the stage table for the Newton
+            // system of this iteration (precompute): A_k, F(s_k, u_k) and the constraint
+            // curvature weighted by the new multipliers of rows k+1
+            T cvk[5] = {0, 0, 0, 0, 0};
             if (!last) {
                 ldn<6>(L.Y(k + 1), yn);
                 up[0] = ld(L.W(k + 1) + 6);
@@ -304,7 +312,27 @@ struct WideSolver {
                 ln.eval(pr.c, w);
                 ln.jac(w, dt, a);
                 ln.next(w, w + 6, dt, Fk);
+                const T v = w[3];
+                cvk[0] = -yn[4] * ln.f2;                                   // Q00
+                cvk[1] = yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;  // Q22
+                cvk[2] = yn[0] * ln.st * dt - yn[1] * ln.ct * dt;          // Q32
+                cvk[3] = yn[4] * v * ln.se * dt;                           // Q55
+                cvk[4] = -yn[4] * ln.ce * dt;                              // Q53
+            } else {
+#pragma unroll
+                for (int j = 0; j < 7; ++j) a[j] = 0;
             }
+            const int sb = L.ST(k);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+            if (!last) {
+                T wn[6];
+                ldn<6>(L.W(k + 1), wn);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, Fk[j] - wn[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cvk[j]);
             if (k >= 1) {
                 um[0] = ld(L.W(k - 1) + 6);
                 um[1] = ld(L.W(k - 1) + 7);
@@ -382,37 +410,27 @@ struct WideSolver {
         ldn<8>(L.ZU(k), zu);
         T g[6];
         grad_state(w, g);
-        T a[7] = {0, 0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
-        T cv[5] = {0, 0, 0, 0, 0};
-        if (!last) {
-            Lin<T> ln;
-            ln.eval(pr.c, w);
-            ln.jac(w, dt, a);
-            if (mode == 0) {
-                T F[6], wn[6], cy[6];
-                ln.next(w, w + 6, dt, F);
-                ldn<6>(L.W(k + 1), wn);
-                ldn<6>(L.Y(k + 1), cy);
-#pragma unroll
-                for (int j = 0; j < 6; ++j) d[j] = F[j] - wn[j];
-                const T v = w[3];
-                cv[0] = -cy[4] * ln.f2;                                   // Q00
-                cv[1] = cy[0] * v * ln.ct * dt + cy[1] * v * ln.st * dt;  // Q22
-                cv[2] = cy[0] * ln.st * dt - cy[1] * ln.ct * dt;          // Q32
-                cv[3] = cy[4] * v * ln.se * dt;                           // Q55
-                cv[4] = -cy[4] * ln.ce * dt;                              // Q53
+        // mode 0: A_k, d_k = F(s_k, u_k) - s_{k+1} and the constraint curvature at this
+        // iterate were stored by the statistics sweep (stats); mode 1 (least squares)
+        // computes A_k and has d = 0, no curvature.
+        if (mode == 1) {
+            T a[7] = {0, 0, 0, 0, 0, 0, 0};
+            if (!last) {
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                ln.jac(w, dt, a);
             }
-        }
 #pragma unroll
-        for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+            for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, 0);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, 0);
+        }
         st(sb + WideLayout::SDT, dt);
         st(sb + WideLayout::SZERO, 0);
         st(sb + WideLayout::SONE, 1);
         st(sb + WideLayout::SMONE, -1);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, d[j]);
-#pragma unroll
-        for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cv[j]);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             T qd, qv;
@@ -481,16 +499,17 @@ struct WideSolver {
     // slot of augmented-state column j among the A_hat columns of G (-1: zero column)
     MPCG_HD static int aslot(int j) { return j < 4 ? j : (j == 5 ? 4 : -1); }
 
-    // Riccati sweep.  Lane (i, j) keeps entry (i, j) of the cost-to-go matrix P (and
-    // p_i) in registers; nothing of P is stored: the forward pass needs only the gains,
-    // and the multipliers come from the adjoint recursion (forward()).
+    // Riccati sweep.  Lane (i, j) owns entry (i, j) of the cost-to-go matrix P (and
+    // keeps p_i); P lives only in a 64-entry scratch for the row reads of the next
+    // stage: the forward pass needs only the gains, and the multipliers come from the
+    // adjoint recursion (forward()).
     MPCG_HD bool riccati(int mode, T delta_w) {
         wv.sync();
         precompute(mode, delta_w);
         typedef WideLayout W_;
         const int i = t >> 3, j = t & 7;
         const int si = aslot(i), sj = aslot(j);
-        const int sm = L.SCR();
+        const int sm = L.SCR(), sp = L.SCR() + 64;
         // per-lane stage-table offsets: G column j, A_hat column i
         int go[8], ao[8];
 #pragma unroll
@@ -520,20 +539,15 @@ struct WideSolver {
             const int sb = L.ST(N - 1);
             Pij = ld(sb + q1);
             pvi = ld(sb + qv);
+            st(sp + t, Pij);
         }
         bool bad = false;  // a stage's reduced Hessian not positive definite
         for (int k = N - 2; k >= 0; --k) {
             const int sb = L.ST(k);
-            // row i of P' from the 8 lanes of the row
+            // row i of P' (16-byte reads of the scratch the previous stage wrote)
             T pr_[8], g[8];
-            pr_[0] = wv.template bcast8<0>(Pij);
-            pr_[1] = wv.template bcast8<1>(Pij);
-            pr_[2] = wv.template bcast8<2>(Pij);
-            pr_[3] = wv.template bcast8<3>(Pij);
-            pr_[4] = wv.template bcast8<4>(Pij);
-            pr_[5] = wv.template bcast8<5>(Pij);
-            pr_[6] = wv.template bcast8<6>(Pij);
-            pr_[7] = wv.template bcast8<7>(Pij);
+            wv.sync();
+            ldv<8>(sp + 8 * i, pr_);
 #pragma unroll
             for (int q = 0; q < 8; ++q) g[q] = ld(sb + go[q]);
             // M = P' G, entry (i, j) per lane; column 7 adds p' (h = P' d + p')
@@ -591,6 +605,7 @@ struct WideSolver {
             }
             Pij = qh + (hj ? a0 + a1 : (T)0) + s0i * K0 + s1i * K1;
             pvi = qvi + (h0 + h1) + s0i * kf0 + s1i * kf1;
+            st(sp + t, Pij);
             if (i == 0) {
                 st(L.KR(k) + j, K0);
                 st(L.KR(k) + 8 + j, K1);
@@ -917,8 +932,8 @@ struct WideSolver {
             if (wv.uni(Emu > kappa_eps * mu || mu <= mu_min)) break;
             const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
             if (wv.uni(mnew >= mu)) break;
-            mu = mnew;
-            tau = tmax((T)0.99, (T)1 - mu);
+            mu = wv.uni_d(mnew);
+            tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
             nf = 0;
         }
         wv.mark(8);
@@ -952,11 +967,15 @@ struct WideSolver {
         const T thetak = theta;
         const T gd = F.gd;
         const int cap = P.filter_cap;
+        // the switching-condition powers are loop invariants of the trial loop
+        T pgd = 0, pth = 0;
+        if (wv.uni(gd < 0)) {
+            pgd = wv.uni_d((T)pow((double)-gd, (double)s_phi));
+            pth = wv.uni_d((T)pow((double)thetak, (double)s_theta));
+        }
         T alpha_min;
         if (gd < 0 && thetak <= theta_min)
-            alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd,
-                                                             delta_sw * (T)pow((double)thetak, (double)s_theta) /
-                                                                 (T)pow((double)-gd, (double)s_phi)));
+            alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd, delta_sw * pth / pgd));
         else if (gd < 0)
             alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
         else
@@ -979,8 +998,7 @@ struct WideSolver {
                     hit = hit || wv.any(h);
                 }
                 if (!hit) {
-                    const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
-                                                 delta_sw * (T)pow((double)thetak, (double)s_theta));
+                    const bool sw = (gd < 0) && (alpha * pgd > delta_sw * pth);
                     if (wv.uni(thetak <= theta_min && sw)) {
                         if (wv.uni(phit <= phik + eta_phi * alpha * gd)) { accepted = true; ftype = true; break; }
                     } else if (wv.uni(thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak)) {

@@ -102,3 +102,39 @@ class BatchSolver:
         _lib.check(_lib.lib().mpcg_solve_device(
             self._h, B, ptr(state), ptr(coeffs), ptr(u0), ptr(traj), ptr(status), ptr(obj), ptr(iters),
             C.c_void_p(stream.cuda_stream)), "mpcg_solve_device")
+
+    # ------------------------------------------------ the caller side on the device
+    def preprocess_device(self, pose, vel, plan, state, coeffs, delay_mode: bool = True, stream=None):
+        """Tracking::findBestPath's preprocessing (driving_state.cpp:175-256) for B robots.
+
+        pose [B,3] (x, y, yaw), vel [B,3] (v feedback, previous w, previous throttle),
+        plan [B,M,2] -> state [B,6], coeffs [B,4]; torch float64 tensors on this GPU."""
+        import torch
+
+        B, M = plan.shape[0], plan.shape[1]
+        for t, shape in ((pose, (B, 3)), (vel, (B, 3)), (plan, (B, M, 2)), (state, (B, 6)), (coeffs, (B, 4))):
+            assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and tuple(t.shape) == shape
+        if stream is None:
+            stream = torch.cuda.current_stream(pose.device)
+        ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        _lib.check(_lib.lib().mpcg_preprocess_device(
+            self._h, B, M, ptr(pose), ptr(vel), ptr(plan), int(bool(delay_mode)), ptr(state), ptr(coeffs),
+            C.c_void_p(stream.cuda_stream)), "mpcg_preprocess_device")
+
+    def track_device(self, pose, vel, plan, cmd, traj=None, status=None, delay_mode: bool = True, stream=None):
+        """One control tick for B robots: preprocessing, solve, post-processing
+        (driving_state.cpp:175-269).  cmd [B,3] = (speed, w, throttle)."""
+        import torch
+
+        B, M = plan.shape[0], plan.shape[1]
+        for t, shape in ((pose, (B, 3)), (vel, (B, 3)), (plan, (B, M, 2)), (cmd, (B, 3))):
+            assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and tuple(t.shape) == shape
+        if traj is not None:
+            assert traj.dtype == torch.float64 and traj.is_contiguous() and traj.numel() == B * 3 * self.N
+        assert status is None or (status.dtype == torch.int32 and status.numel() == B)
+        if stream is None:
+            stream = torch.cuda.current_stream(pose.device)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        _lib.check(_lib.lib().mpcg_track_device(
+            self._h, B, M, ptr(pose), ptr(vel), ptr(plan), int(bool(delay_mode)), ptr(cmd), ptr(traj), ptr(status),
+            C.c_void_p(stream.cuda_stream)), "mpcg_track_device")

@@ -63,6 +63,7 @@ struct HostWave {
         return r;
     }
     double dn1(double v) const { return from(v, t < 63 ? t + 1 : t); }
+    double uni_d(double v) const { return from(v, 0); }
     template <int q>
     double bcast8(double v) const { return from(v, (t & ~7) | q); }
     // reduction partners of the device (wave_dev.h): xor 1, xor 2, mirror 8, mirror 16, xor 16, xor 32

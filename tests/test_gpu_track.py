@@ -1,0 +1,161 @@
+"""GPU: the caller side of MPC::Solve on the device -- Tracking::findBestPath's
+preprocessing (mpcg_preprocess_device) and the whole control tick (mpcg_track_device:
+preprocessing, solve, post-processing of driving_state.cpp:262-269).
+
+References: the oracle's restatement (oracle/preprocess.c) and its committed fixtures
+(tests/golden/preprocess.npz), the vectorised NumPy version used to build the
+benchmark inputs (mpc_ros_amd/infinity.py), and the oracle's solve.  Tolerance: the
+Householder QR runs in the oracle's operation order (differences are FMA contraction
+only), 1e-11 on state/coeffs; the tick's commands at the solve's 1e-7.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import load_npz
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test without a GPU")
+    return torch
+
+
+def _solver(P=None):
+    from mpc_ros_amd import params
+    from mpc_ros_amd.solver import BatchSolver
+
+    return BatchSolver(0, P or params.PLUGIN_DEFAULTS)
+
+
+def _run_preprocess(torch, s, pose, vel, plan, delay=True):
+    dev = torch.device("cuda:0")
+    B = pose.shape[0]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+    st = torch.empty((B, 6), dtype=torch.float64, device=dev)
+    cf = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    s.preprocess_device(t(pose), t(vel), t(plan), st, cf, delay_mode=delay)
+    torch.cuda.synchronize()
+    return st.cpu().numpy(), cf.cpu().numpy()
+
+
+def test_preprocess_matches_oracle_fixtures(torch_cuda):
+    g = load_npz("preprocess.npz")
+    from mpc_ros_amd import params
+
+    s = _solver(dict(params.PLUGIN_DEFAULTS, DT=float(g["dt"])))
+    st, cf = _run_preprocess(torch_cuda, s, g["pose"], g["vel"], g["plan"])
+    np.testing.assert_allclose(cf, g["coeffs"], rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(st, g["state"], rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("delay", [True, False])
+def test_preprocess_matches_benchmark_generator(torch_cuda, delay):
+    from mpc_ros_amd import infinity
+
+    idx = np.arange(1000, 1000 + 4096)
+    sc = infinity.draw_scenarios(idx)
+    px, py, yaw, plan = infinity.scenario_poses(sc)
+    ref_st, ref_cf = infinity.find_best_path(px, py, yaw, sc["v"], sc["w_prev"], sc["a_prev"], 0.1, plan, delay)
+    pose = np.stack([px, py, yaw], axis=1)
+    vel = np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], axis=1)
+    st, cf = _run_preprocess(torch_cuda, _solver(), pose, vel, plan, delay)
+    np.testing.assert_allclose(cf, ref_cf, rtol=1e-9, atol=1e-10)
+    np.testing.assert_allclose(st, ref_st, rtol=1e-9, atol=1e-10)
+
+
+def test_preprocess_rejects_short_plans(torch_cuda):
+    """polyfit asserts order 3 <= M - 1 (driving_state.cpp:286): M < 4 is an API error."""
+    from mpc_ros_amd._lib import MpcgError
+
+    pose = np.zeros((2, 3))
+    with pytest.raises(MpcgError):
+        _run_preprocess(torch_cuda, _solver(), pose, pose, np.zeros((2, 3, 2)))
+
+
+@pytest.mark.parametrize("M", [4, 11, 17, 40, 64])
+def test_preprocess_plan_lengths(torch_cuda, oracle, M):
+    """Short, medium and long plans (M > 16 takes the 64-row kernel) against the oracle."""
+    rng = np.random.default_rng(M)
+    B = 96
+    pose = np.stack([rng.uniform(-2, 2, B), rng.uniform(-2, 2, B), rng.uniform(-np.pi, np.pi, B)], axis=1)
+    vel = np.stack([rng.uniform(0, 0.8, B), rng.uniform(-1, 1, B), rng.uniform(-1, 1, B)], axis=1)
+    s = np.linspace(0.0, 5.0, M)
+    plan = np.empty((B, M, 2))
+    for b in range(B):
+        h0, k0 = rng.uniform(-np.pi, np.pi), rng.uniform(-0.4, 0.4)
+        hd = h0 + k0 * s
+        plan[b, :, 0] = pose[b, 0] + rng.uniform(-0.3, 0.3) + np.cumsum(np.cos(hd)) * (s[1] - s[0] if M > 1 else 0)
+        plan[b, :, 1] = pose[b, 1] + rng.uniform(-0.3, 0.3) + np.cumsum(np.sin(hd)) * (s[1] - s[0] if M > 1 else 0)
+    st, cf = _run_preprocess(torch_cuda, _solver(), pose, vel, plan)
+    for b in range(B):
+        rc, ost, ocf = oracle.find_best_path(*pose[b], *vel[b], 0.1, plan[b], True)
+        assert rc == 0
+        np.testing.assert_allclose(cf[b], ocf, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(st[b], ost, rtol=1e-9, atol=1e-9)
+
+
+def test_track_tick_matches_oracle_pipeline(torch_cuda, oracle):
+    """cmd = (speed, w, throttle) of one control tick against oracle preprocessing +
+    oracle solve + driving_state.cpp:262-269."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity, params
+
+    P = params.PLUGIN_DEFAULTS
+    idx = np.arange(5000, 5000 + 64)
+    sc = infinity.draw_scenarios(idx)
+    px, py, yaw, plan = infinity.scenario_poses(sc)
+    pose = np.stack([px, py, yaw], axis=1)
+    vel = np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], axis=1)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+    B = len(idx)
+    cmd = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    _solver(P).track_device(t(pose), t(vel), t(plan), cmd, status=status)
+    torch.cuda.synchronize()
+    cmd = cmd.cpu().numpy()
+    sts, cfs = [], []
+    for b in range(B):
+        rc, ost, ocf = oracle.find_best_path(*pose[b], *vel[b], P["DT"], plan[b], True)
+        assert rc == 0
+        sts.append(ost)
+        cfs.append(ocf)
+    ref = oracle.mpc_solve_batch(P, np.array(sts), np.array(cfs), opts=oracle.ipm_opts(tol=1e-8), nthreads=16)
+    w = ref["u0"][:, 0]
+    thr = ref["u0"][:, 1]
+    speed = np.minimum(vel[:, 0] + thr * P["DT"], P["REF_V"])
+    np.testing.assert_allclose(cmd[:, 1], w, atol=1e-7)
+    np.testing.assert_allclose(cmd[:, 2], thr, atol=1e-7)
+    np.testing.assert_allclose(cmd[:, 0], speed, atol=1e-7)
+    np.testing.assert_array_equal(status.cpu().numpy(), ref["status"])
+
+
+def test_track_tick_equals_solve_on_preprocessed_inputs(torch_cuda):
+    """At the benchmark size: the fused tick's controls equal a solve of the
+    separately preprocessed problems (same kernels, same inputs)."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity
+
+    B = 65536
+    sc = infinity.draw_scenarios(np.arange(B))
+    px, py, yaw, plan = infinity.scenario_poses(sc)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+    pose, vel, tplan = t(np.stack([px, py, yaw], 1)), t(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1)), t(plan)
+    s = _solver()
+    cmd = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    s.track_device(pose, vel, tplan, cmd)
+    st = torch.empty((B, 6), dtype=torch.float64, device=dev)
+    cf = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    s.preprocess_device(pose, vel, tplan, st, cf)
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+    s.solve_device(st, cf, u0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cmd[:, 1:].cpu().numpy(), u0.cpu().numpy())
