@@ -265,28 +265,28 @@ struct WideSolver {
 
     MPCG_HD void stats(bool acc, T alpha, T amax_z) {
         wv.sync();
-        if (acc && t < N) {
-            const int k = t;
-            const bool last = k == N - 1;
-            T w[8], dw[8], zl[8], zu[8], y[6], yp[6];
-            ldn<8>(L.W(k), w);
-            ldn<8>(L.DW(k), dw);
-            ldn<8>(L.ZL(k), zl);
-            ldn<8>(L.ZU(k), zu);
-            ldn<6>(L.Y(k), y);
-            ldn<6>(L.YP(k), yp);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (!(last && j >= 6)) {
+        if (acc) {
+            // element-parallel: element e = 8k + j of the stage-major arrays, 64 per round
+            // (bounds selected among locals: a select between member addresses would
+            // force the solver object into scratch)
+            const T bl[3] = {sl, wl, al}, bh[3] = {su, wu, au};
+            for (int e = t; e < 8 * N; e += 64) {
+                const int k = e >> 3, j = e & 7;
+                const T lo = j < 6 ? bl[0] : (j == 6 ? bl[1] : bl[2]);
+                const T hi = j < 6 ? bh[0] : (j == 6 ? bh[1] : bh[2]);
+                if (!(k == N - 1 && j >= 6)) {
                     T wn, zln, zun;
-                    accept_one(w[j], dw[j], zl[j], zu[j], vlo(j), vhi(j), alpha, amax_z, &wn, &zln, &zun);
-                    st(L.W(k) + j, wn);
-                    st(L.ZL(k) + j, zln);
-                    st(L.ZU(k) + j, zun);
+                    accept_one(ld(L.W(0) + e), ld(L.DW(0) + e), ld(L.ZL(0) + e), ld(L.ZU(0) + e), lo, hi,
+                               alpha, amax_z, &wn, &zln, &zun);
+                    st(L.W(0) + e, wn);
+                    st(L.ZL(0) + e, zln);
+                    st(L.ZU(0) + e, zun);
+                }
+                if (j < 6) {
+                    const T y = ld(L.Y(0) + e), yp = ld(L.YP(0) + e);
+                    st(L.Y(0) + e, y + alpha * (yp - y));
                 }
             }
-#pragma unroll
-            for (int j = 0; j < 6; ++j) st(L.Y(k) + j, y[j] + alpha * (yp[j] - y[j]));
         }
         wv.sync();
         T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
