@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--profile-name", default=None, help="PMC summary to read traffic from")
     ap.add_argument("--strategy", default="auto", choices=["auto", "lane", "wave"],
                     help="kernel strategy: one problem per lane / per wavefront")
+    ap.add_argument("--model", default="diffdrive", choices=["diffdrive", "bicycle"],
+                    help="dynamics: FG_eval's differential drive, or the kinematic bicycle (BASELINE configs[4]: "
+                         "run with --horizon 25)")
     ap.add_argument("--mode", default="solve", choices=["solve", "track"],
                     help="solve: MPC::Solve on preprocessed inputs (the metric); track: the whole control "
                          "tick from raw poses and waypoint plans (findBestPath + solve + post-processing)")
@@ -109,6 +112,8 @@ def main():
     B = a.batch
     total = B * world
     P = dict(params.PLUGIN_DEFAULTS, STEPS=N)
+    if a.model == "bicycle":  # steering bound 0.5 rad, wheelbase 0.5 m (tests/golden/bicycle_N25.npz)
+        P.update(MODEL=1, LF=0.5, ANGVEL=0.5)
     start, count = D.shard(total, rank, world)
     st, cf = infinity.make_problems(np.arange(start, start + count))
     tst = torch.from_numpy(st).to(dev)
@@ -197,10 +202,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem)",
-            "config": {"workload": f"diff-drive NMPC (MPC::Solve NLP, Ipopt algorithm), N={N}, fp64, "
+            "config": {"workload": f"{'diff-drive' if a.model == 'diffdrive' else 'kinematic-bicycle'} NMPC "
+                                   f"(MPC::Solve NLP, Ipopt algorithm), N={N}, fp64, "
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
                        "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}",
-                       "mode": a.mode},
+                       "mode": a.mode, "model": a.model},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mpcg::k_solve_wide" if solver.strategy == "wave" else "lane kernels",

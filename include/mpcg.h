@@ -41,7 +41,9 @@ extern "C" {
  * leaves at their defaults (mpc_planner.cpp:356-368). */
 typedef struct mpcg_params {
     int32_t steps;            /* "STEPS": horizon N (double truncated to int, :74, :247) */
-    int32_t model;            /* 0 = differential drive (FG_eval); 1 = kinematic bicycle */
+    int32_t model;            /* 0 = differential drive (FG_eval); 1 = kinematic bicycle: the control
+                                 w is the steering angle (|w| <= ANGVEL) and the heading rows turn
+                                 by v w / wheelbase dt (strategy WAVE only) */
     double dt;                /* "DT" */
     double ref_cte;           /* "REF_CTE" */
     double ref_etheta;        /* "REF_ETHETA" */
@@ -75,7 +77,8 @@ const char* mpcg_last_error(void);
 int mpcg_params_default(mpcg_params* p);
 /* Defaults the move_base plugin loads (mpc_ros/cfg/MPCPlanner.cfg:22-37, DT 0.1). */
 int mpcg_params_plugin_default(mpcg_params* p);
-/* One LoadParams map entry: key is one of the 15 reference keys.
+/* One LoadParams map entry: key is one of the 15 reference keys, or one of the
+ * extension keys MODEL (0 differential drive, 1 kinematic bicycle) and LF (wheelbase).
  * Returns 0 if applied, 1 if the key is unknown (ignored, as LoadParams ignores it). */
 int mpcg_params_set(mpcg_params* p, const char* key, double value);
 /* Validate a parameter set (steps >= 2, dt > 0, bounds > 0, weights >= 0). */

@@ -57,6 +57,8 @@ struct IpmParams {
     double mu_init;             // Ipopt default 0.1
     int max_iter;               // Ipopt default 3000
     int filter_cap;             // filter entries kept per problem
+    int model;                  // 0 differential drive (FG_eval), 1 kinematic bicycle (wide solver only)
+    double lf;                  // model 1: wheelbase [m]
 };
 
 // Status numbering of CppAD::ipopt::solve_result::status_type

@@ -121,6 +121,9 @@ int mpcg_params_set(mpcg_params* p, const char* key, double v) {
     else if (k == "ANGVEL") p->max_angvel = v;
     else if (k == "MAXTHR") p->max_throttle = v;
     else if (k == "BOUND") p->bound = v;
+    // extension keys (not in the reference map): dynamics model and wheelbase
+    else if (k == "MODEL") p->model = (int32_t)v;
+    else if (k == "LF") p->wheelbase = v;
     else return 1;
     return 0;
 }
@@ -137,7 +140,8 @@ int mpcg_params_check(const mpcg_params* p) {
     if (p->max_iter < 0) return fail(-1, "max_iter must be >= 0");
     if (p->filter_cap < 1 || p->filter_cap > 1024) return fail(-1, "filter_cap must be in [1, 1024]");
     if (!(p->bound_relax_factor >= 0) || !(p->mu_init > 0)) return fail(-1, "invalid Ipopt options");
-    if (p->model != 0) return fail(-1, "model: only 0 (differential drive) is implemented");
+    if (p->model != 0 && p->model != 1) return fail(-1, "model must be 0 (differential drive) or 1 (bicycle)");
+    if (p->model == 1 && !(p->wheelbase > 0)) return fail(-1, "model 1 needs wheelbase (LF) > 0");
     return 0;
 }
 
@@ -163,6 +167,8 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
     q.mu_init = p.mu_init;
     q.max_iter = p.max_iter;
     q.filter_cap = p.filter_cap;
+    q.model = p.model;
+    q.lf = p.wheelbase;
     return q;
 }
 
@@ -294,6 +300,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
         if (e != hipSuccess) return hip_fail(e, "wide solve launch");
         return 0;
     }
+    if (P.model != 0) return fail(-1, "the bicycle model runs on strategy WAVE only (steps <= 64)");
     rc = ensure_ws(h, B);
     if (rc) return rc;
     e = mpcg::launch_ipm_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,

@@ -26,6 +26,7 @@ struct WideArgs {
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
 // budget of 256 per lane lets all of them be resident
+template <int MODEL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     const int64_t p = blockIdx.x;
     if (p >= a.B) return;
@@ -37,7 +38,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int j = 0; j < 4; ++j) pr.c[j] = a.coeffs[p * 4 + j];
     DevWave wv;
     wv.t = t;
-    WideSolver<DevWave> S(a.P, pr, wv);
+    WideSolver<DevWave, MODEL> S(a.P, pr, wv);
     S.solve();
     const double o = S.objective_out();
     const int N = a.P.N;
@@ -62,11 +63,14 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
                              double* traj, int32_t* status, double* obj, int32_t* iters, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
     const size_t lds = wide_lds_bytes(P);
-    hipError_t e = hipFuncSetAttribute((const void*)k_solve_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    const void* fn = P.model == 1 ? (const void*)k_solve_wide<1> : (const void*)k_solve_wide<0>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, state, coeffs, u0, traj, status, obj, iters};
-    hipLaunchKernelGGL(k_solve_wide, dim3((unsigned)B), dim3(64), lds, stream, a);
+    if (P.model == 1)
+        hipLaunchKernelGGL(k_solve_wide<1>, dim3((unsigned)B), dim3(64), lds, stream, a);
+    else
+        hipLaunchKernelGGL(k_solve_wide<0>, dim3((unsigned)B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 

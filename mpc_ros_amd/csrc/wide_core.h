@@ -40,7 +40,7 @@ namespace mpcg {
 // LDS layout of one problem (doubles).
 struct WideLayout {
     int N, cap;
-    static constexpr int SS = 44;  // stage table stride
+    static constexpr int SS = 46;  // stage table stride
     // stage table entries
     static constexpr int SA = 0;    // a[7]: non-trivial entries of A_k (Lin::jac)
     static constexpr int SDT = 7;   // dt
@@ -51,6 +51,10 @@ struct WideLayout {
     static constexpr int SCV = 32;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
     static constexpr int SCC = 37;  // rate coupling C0 C1
     static constexpr int SZERO = 39, SONE = 40, SMONE = 41;  // constants 0, 1, -1
+    // model terms of the heading rows (th, eth): d(turn)/d(w) (B_hat column w: dt for the
+    // differential drive, v/lf dt for the bicycle), d(turn)/d(v) (A_hat column v: 0, w/lf dt),
+    // and the (v, w) curvature of the Lagrangian (0, -(y_th + y_eth)/lf dt)
+    static constexpr int STW = 42, STV = 43, SHVD = 44;
     MPCG_HD int W(int k) const { return 8 * k; }
     MPCG_HD int ZL(int k) const { return 8 * N + 8 * k; }
     MPCG_HD int ZU(int k) const { return 16 * N + 8 * k; }
@@ -60,13 +64,15 @@ struct WideLayout {
     MPCG_HD int KR(int k) const { return 48 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
     MPCG_HD int ST(int k) const { return 64 * N + SS * k; }
     // scratch of the Riccati sweep: M^T (M[r][c] at 8 c + r), then P row-major
-    MPCG_HD int SCR() const { return 108 * N; }
-    MPCG_HD int RSC() const { return 108 * N + 128; }  // row scales: ra[6] rb[6] 1.0 (+pad)
-    MPCG_HD int FI() const { return 108 * N + 144; }
-    MPCG_HD int total() const { return 108 * N + 144 + 2 * cap; }
+    MPCG_HD int SCR() const { return (64 + SS) * N; }
+    MPCG_HD int RSC() const { return (64 + SS) * N + 128; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int FI() const { return (64 + SS) * N + 144; }
+    MPCG_HD int total() const { return (64 + SS) * N + 144 + 2 * cap; }
 };
 
-template <class WV>
+// MODEL: 0 differential drive (FG_eval), 1 kinematic bicycle -- a template parameter
+// so that the differential-drive kernel carries none of the bicycle's terms.
+template <class WV, int MODEL = 0>
 struct WideSolver {
     typedef double T;
     const IpmParams P;
@@ -83,9 +89,33 @@ struct WideSolver {
     // line-search / iteration state
     T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt;
     int iter, nf, status;
+    static constexpr int model = MODEL;
+    T lf;  // model 1: wheelbase
 
     MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_)
-        : P(P_), pr(pr_), wv(wv_), L{P_.N, P_.filter_cap}, N(P_.N), t(wv_.t), dt((T)P_.dt) {}
+        : P(P_), pr(pr_), wv(wv_), L{P_.N, P_.filter_cap}, N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf) {}
+
+    // ------------------------------------------------------ the model
+    // F(s, u): FG_eval's dynamics (Lin::next); for the bicycle the heading rows turn by
+    // v w / lf dt instead of w dt (oracle/nlp_mpc.c, same operation order).
+    MPCG_HD void next_m(const Lin<T>& ln, const T* s, const T* u, T* out) const {
+        ln.next(s, u, dt, out);
+        if (model == 1) {
+            const T turn = s[3] * u[0] / lf * dt;
+            out[2] = s[2] + turn;
+            out[5] = s[5] + turn;
+        }
+    }
+    // d(turn)/d(w) and d(turn)/d(v)
+    MPCG_HD void turn_d(const T* s, const T* u, T* tw, T* tv) const {
+        if (model == 1) {
+            *tw = s[3] / lf * dt;
+            *tv = u[0] / lf * dt;
+        } else {
+            *tw = dt;
+            *tv = 0;
+        }
+    }
 
     // ------------------------------------------------------------ LDS helpers
     MPCG_HD T ld(int i) const { return wv.S()[i]; }
@@ -190,10 +220,14 @@ struct WideSolver {
         T m[6];
         m[0] = tmax((T)1, tmax((T)fabs(s[3] * ln.st * dt), (T)fabs(ln.ct * dt)));
         m[1] = tmax((T)1, tmax((T)fabs(s[3] * ln.ct * dt), (T)fabs(ln.st * dt)));
-        m[2] = tmax((T)1, dt);
+        // heading rows: the turn's derivatives at the start point (controls there are 0)
+        T tw, tv;
+        const T u0[2] = {0, 0};
+        turn_d(s, u0, &tw, &tv);
+        m[2] = tmax((T)1, tmax((T)fabs(tw), (T)fabs(tv)));
         m[3] = tmax((T)1, dt);
         m[4] = tmax(tmax((T)1, (T)fabs(ln.f1)), tmax((T)fabs(ln.se * dt), (T)fabs(s[3] * ln.ce * dt)));
-        m[5] = tmax((T)1, dt);
+        m[5] = m[2];
 #pragma unroll
         for (int j = 0; j < 6; ++j) rs[j] = m[j] > (T)100 ? (T)100 / m[j] : (T)1;
     }
@@ -293,6 +327,7 @@ struct WideSolver {
           lg = 0;
         T Fk[6] = {0, 0, 0, 0, 0, 0};
         T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[7];
+        T twk = dt, tvk = 0, hvdk = 0;
         const int k = t;
         const bool act = t < N, last = k == N - 1;
         if (act) {
@@ -304,6 +339,9 @@ struct WideSolver {
             // system of this iteration (precompute): A_k, F(s_k, u_k) and the constraint
             // curvature weighted by the new multipliers of rows k+1
             T cvk[5] = {0, 0, 0, 0, 0};
+            twk = dt;
+            tvk = 0;
+            hvdk = 0;
             if (!last) {
                 ldn<6>(L.Y(k + 1), yn);
                 up[0] = ld(L.W(k + 1) + 6);
@@ -311,7 +349,9 @@ struct WideSolver {
                 Lin<T> ln;
                 ln.eval(pr.c, w);
                 ln.jac(w, dt, a);
-                ln.next(w, w + 6, dt, Fk);
+                next_m(ln, w, w + 6, Fk);
+                turn_d(w, w + 6, &twk, &tvk);
+                if (model == 1) hvdk = -(yn[2] + yn[5]) / lf * dt;
                 const T v = w[3];
                 cvk[0] = -yn[4] * ln.f2;                                   // Q00
                 cvk[1] = yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;  // Q22
@@ -333,6 +373,9 @@ struct WideSolver {
             }
 #pragma unroll
             for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cvk[j]);
+            st(sb + WideLayout::STW, twk);
+            st(sb + WideLayout::STV, tvk);
+            st(sb + WideLayout::SHVD, hvdk);
             if (k >= 1) {
                 um[0] = ld(L.W(k - 1) + 6);
                 um[1] = ld(L.W(k - 1) + 7);
@@ -357,10 +400,11 @@ struct WideSolver {
             grad_state(w, g);
             if (!last) {
                 AT_mul(a, yn, at);
+                if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
                 grad_ctrl(k, um, w + 6, up, gu);
                 f += cost_ctrl(k, w + 6, up);
             }
-            const T btw = dt * (yn[2] + yn[5]), bta = dt * yn[3];
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
             const int nv = last ? 6 : 8;
             T slackprod = 1;
 #pragma unroll
@@ -414,14 +458,18 @@ struct WideSolver {
         // iterate were stored by the statistics sweep (stats); mode 1 (least squares)
         // computes A_k and has d = 0, no curvature.
         if (mode == 1) {
-            T a[7] = {0, 0, 0, 0, 0, 0, 0};
+            T a[7] = {0, 0, 0, 0, 0, 0, 0}, tw = dt, tv = 0;
             if (!last) {
                 Lin<T> ln;
                 ln.eval(pr.c, w);
                 ln.jac(w, dt, a);
+                turn_d(w, w + 6, &tw, &tv);
             }
 #pragma unroll
             for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+            st(sb + WideLayout::STW, tw);
+            st(sb + WideLayout::STV, tv);
+            st(sb + WideLayout::SHVD, 0);
 #pragma unroll
             for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, 0);
 #pragma unroll
@@ -488,10 +536,10 @@ struct WideSolver {
         o = (s == 0) ? (m == 0 ? O : (m == 4 ? A + 4 : Z)) : o;
         o = (s == 1) ? (m == 1 ? O : (m == 4 ? W_::SMONE : Z)) : o;
         o = (s == 2) ? (m == 0 ? A + 0 : (m == 1 ? A + 2 : (m == 2 ? O : Z))) : o;
-        o = (s == 3) ? (m == 0 ? A + 1 : (m == 1 ? A + 3 : (m == 3 ? O : (m == 4 ? A + 5 : Z)))) : o;
+        o = (s == 3) ? (m == 0 ? A + 1 : (m == 1 ? A + 3 : (m == 3 ? O : (m == 4 ? A + 5 : ((m == 2 || m == 5) ? W_::STV : Z))))) : o;
         o = (s == 4) ? (m == 4 ? A + 6 : (m == 5 ? O : Z)) : o;
-        // B_hat: w -> dt e2 + dt e5 + e6 ; a -> dt e3 + e7
-        o = (s == 5) ? ((m == 2 || m == 5) ? W_::SDT : (m == 6 ? O : Z)) : o;
+        // B_hat: w -> tw e2 + tw e5 + e6 (tw = d turn / d w) ; a -> dt e3 + e7
+        o = (s == 5) ? ((m == 2 || m == 5) ? W_::STW : (m == 6 ? O : Z)) : o;
         o = (s == 6) ? (m == 3 ? W_::SDT : (m == 7 ? O : Z)) : o;
         o = (s == 7) ? (m < 6 ? D + m : Z) : o;
         return o;
@@ -522,6 +570,8 @@ struct WideSolver {
         const int mj = sm + 8 * (hj ? sj : 0), mi = sm + 8 * (hi ? si : 0);
         const int c0j = j == 6 ? W_::SCC : W_::SZERO, c1j = j == 7 ? W_::SCC + 1 : W_::SZERO;
         const int c0i = i == 6 ? W_::SCC : W_::SZERO, c1i = i == 7 ? W_::SCC + 1 : W_::SZERO;
+        // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
+        const int hvj = j == 3 ? W_::SHVD : W_::SZERO, hvi = i == 3 ? W_::SHVD : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
         const int q1 = (i == j && i < 6) ? W_::SQD + i : W_::SZERO;
         int q2 = W_::SZERO;
@@ -574,21 +624,23 @@ struct WideSolver {
             ld2(sb + W_::SQD + 6, qd6, qd7);
             ld2(sb + W_::SQV + 6, qv6, qv7);
             const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
+            const T hv0j = model == 1 ? ld(sb + hvj) : (T)0, hv0i = model == 1 ? ld(sb + hvi) : (T)0;
+            const T tw = model == 1 ? ld(sb + W_::STW) : dt;
             const T qh = ld(sb + q1) + ld(sb + q2);
             const T qvi = ld(sb + qv);
             // R_tilde = R + B^T P' B, r_tilde = r + B^T h, S_tilde = B^T P' A (+ rate coupling)
-            const T Rt00 = qd6 + (dt * (m25 + m55) + m65);
-            const T Rt01 = dt * (m26 + m56) + m66;
+            const T Rt00 = qd6 + (tw * (m25 + m55) + m65);
+            const T Rt01 = tw * (m26 + m56) + m66;
             const T Rt11 = qd7 + (dt * m36 + m76);
             const T det = Rt00 * Rt11 - Rt01 * Rt01;
             bad = bad || !(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11);
-            const T rt0 = qv6 + (dt * (m7[2] + m7[5]) + m7[6]);
+            const T rt0 = qv6 + (tw * (m7[2] + m7[5]) + m7[6]);
             const T rt1 = qv7 + (dt * m7[3] + m7[7]);
             const T rdet = rcp(det);
             const T i00 = Rt11 * rdet, i01 = -Rt01 * rdet, i11 = Rt00 * rdet;
-            const T s0j = hj ? dt * (mc[2] + mc[5]) + mc[6] : cc0j;
+            const T s0j = (hj ? tw * (mc[2] + mc[5]) + mc[6] : cc0j) + hv0j;
             const T s1j = hj ? dt * mc[3] + mc[7] : cc1j;
-            const T s0i = hi ? dt * (mi2 + mi5) + mi6 : cc0i;
+            const T s0i = (hi ? tw * (mi2 + mi5) + mi6 : cc0i) + hv0i;
             const T s1i = hi ? dt * mi3 + mi7 : cc1i;
             const T K0 = -(i00 * s0j + i01 * s1j);
             const T K1 = -(i01 * s0j + i11 * s1j);
@@ -647,12 +699,13 @@ struct WideSolver {
         // systolically: lane k holds stage k's records, every step every lane applies its
         // own stage map to the vector it holds and passes the result one lane up, so lane
         // k sees its correct input at step k (and keeps it).
-        T K[16], kf[2], a[8], d[6];
+        T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
         if (t < N - 1) {
             ldv<16>(L.KR(t), K);
             ldv<2>(L.ST(t) + WideLayout::SKF, kf);
             ldv<8>(L.ST(t) + WideLayout::SA, a);
             ldv<6>(L.ST(t) + WideLayout::SD, d);
+            ld2(L.ST(t) + WideLayout::STW, twl, tvl);
         } else {  // last stage (and idle lanes): no control, du = 0
 #pragma unroll
             for (int q = 0; q < 16; ++q) K[q] = 0;
@@ -694,9 +747,11 @@ struct WideSolver {
             }
             T y[8];
             A_mul(a, x, y);
-            y[2] += dt * du0;
+            y[2] += tvl * x[3];
+            y[5] += tvl * x[3];
+            y[2] += twl * du0;
             y[3] += dt * du1;
-            y[5] += dt * du0;
+            y[5] += twl * du0;
 #pragma unroll
             for (int j = 0; j < 6; ++j) y[j] += d[j];
             y[6] = du0;
@@ -719,15 +774,17 @@ struct WideSolver {
         // (rows 0..5 of the Riccati costate P_k ds_k + p_k), a backward systolic pass:
         // lane k holds stage k's Hessian diagonal and curvature, gradient and A_k.
         wv.mark(3);
-        T lam[6], lk[6], base[6], ak[8];
+        T lam[6], lk[6], base[6], ak[8], tva = 0;
         {
-            T qd[8], qv[8], cv[6];
+            T qd[8], qv[8], cv[6], hvd = 0;
             if (t < N) {
                 const int sb = L.ST(t);
                 ldv<8>(sb + WideLayout::SQD, qd);
                 ldv<8>(sb + WideLayout::SQV, qv);
                 ldv<6>(sb + WideLayout::SCV, cv);  // cv[0..4] = Q00 Q22 Q32 Q55 Q53
                 ldv<8>(sb + WideLayout::SA, ak);
+                tva = ld(sb + WideLayout::STV);
+                hvd = ld(sb + WideLayout::SHVD);
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) { qd[q] = 0; qv[q] = 0; ak[q] = 0; }
@@ -741,12 +798,14 @@ struct WideSolver {
             base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
             base[4] = qd[4] * x[4] + qv[4];
             base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
+            base[3] += hvd * duk[0];  // (v, w) curvature times the stage's w step (bicycle)
         }
 #pragma unroll
         for (int q = 0; q < 6; ++q) { lam[q] = 0; lk[q] = 0; }
         for (int s = N - 1; s >= 0; --s) {
             T o[6];
             AT_mul(ak, lam, o);
+            o[3] += tva * (lam[2] + lam[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) o[q] += base[q];
             if (t == s) {
@@ -843,7 +902,7 @@ struct WideSolver {
                 f += cost_ctrl(k, w + 6, up);
                 Lin<T> ln;
                 ln.eval(pr.c, w);
-                ln.next(w, w + 6, dt, Fk);
+                next_m(ln, w, w + 6, Fk);
             }
         }
         T Fprev[6];

@@ -17,6 +17,8 @@
  *   th1 - (th0 + w0 dt)              v1 - (v0 + a0 dt)
  *   cte1 - ((f(x0) - y0) + v0 sin(eth0) dt)      eth1 - (eth0 + w0 dt)
  * The dead trj_grad0 = atan(f'(x0)) (:192-198) does not reach fg and is omitted.
+ * model 1 (kinematic bicycle, ora.h): w is the steering angle delta and the heading
+ * rows are th1 - (th0 + v0 * delta0 / lf * dt), eth1 - (eth0 + v0 * delta0 / lf * dt).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -83,10 +85,11 @@ void ora_mpc_fg(const ora_mpc_params* p, const double* c, const double* v, doubl
         double w0 = v[IW(N) + i], a0 = v[IA(N) + i];
         g[0 * N + i + 1] = v[IX(N) + i + 1] - (x0 + v0 * cos(th0) * dt);
         g[1 * N + i + 1] = v[IY(N) + i + 1] - (y0 + v0 * sin(th0) * dt);
-        g[2 * N + i + 1] = v[ITH(N) + i + 1] - (th0 + w0 * dt);
+        const double turn = p->model == 1 ? v0 * w0 / p->lf * dt : w0 * dt;
+        g[2 * N + i + 1] = v[ITH(N) + i + 1] - (th0 + turn);
         g[3 * N + i + 1] = v[IV(N) + i + 1] - (v0 + a0 * dt);
         g[4 * N + i + 1] = v[ICTE(N) + i + 1] - ((fpoly(c, x0) - y0) + v0 * sin(eth0) * dt);
-        g[5 * N + i + 1] = v[IETH(N) + i + 1] - (eth0 + w0 * dt);
+        g[5 * N + i + 1] = v[IETH(N) + i + 1] - (eth0 + turn);
     }
 }
 
@@ -134,10 +137,15 @@ void ora_mpc_jac_g(const ora_mpc_params* p, const double* c, const double* v, do
         JJ(r, IY(N) + i) = -1.0;
         JJ(r, ITH(N) + i) = -v0 * cos(th0) * dt;
         JJ(r, IV(N) + i) = -sin(th0) * dt;
+        const double w0 = v[IW(N) + i];
+        /* d(turn)/d(w), d(turn)/d(v) */
+        const double tw = p->model == 1 ? v0 / p->lf * dt : dt;
+        const double tv = p->model == 1 ? w0 / p->lf * dt : 0.0;
         r = 2 * N + i + 1;
         JJ(r, ITH(N) + i + 1) = 1.0;
         JJ(r, ITH(N) + i) = -1.0;
-        JJ(r, IW(N) + i) = -dt;
+        JJ(r, IW(N) + i) = -tw;
+        if (p->model == 1) JJ(r, IV(N) + i) = -tv;
         r = 3 * N + i + 1;
         JJ(r, IV(N) + i + 1) = 1.0;
         JJ(r, IV(N) + i) = -1.0;
@@ -151,7 +159,8 @@ void ora_mpc_jac_g(const ora_mpc_params* p, const double* c, const double* v, do
         r = 5 * N + i + 1;
         JJ(r, IETH(N) + i + 1) = 1.0;
         JJ(r, IETH(N) + i) = -1.0;
-        JJ(r, IW(N) + i) = -dt;
+        JJ(r, IW(N) + i) = -tw;
+        if (p->model == 1) JJ(r, IV(N) + i) = -tv;
     }
 #undef JJ
 }
@@ -194,6 +203,11 @@ void ora_mpc_hess(const ora_mpc_params* p, const double* c, const double* v, dou
         HADD(IX(N) + i, IX(N) + i, -lc * fpoly_d2(c, x0));
         HADD(IETH(N) + i, IETH(N) + i, lc * v0 * sin(eth0) * dt);
         HADD(IETH(N) + i, IV(N) + i, -lc * cos(eth0) * dt);
+        if (p->model == 1) {
+            /* heading rows: -(v delta / lf) dt */
+            const double lt = lam[2 * N + i + 1], le = lam[5 * N + i + 1];
+            HADD(IW(N) + i, IV(N) + i, -(lt + le) / p->lf * dt);
+        }
     }
 #undef HADD
 #undef HH

@@ -93,6 +93,13 @@ typedef struct ora_mpc_params {
     double dt, ref_cte, ref_etheta, ref_v;
     double w_cte, w_etheta, w_v, w_angvel, w_accel, w_angvel_d, w_accel_d;
     double max_angvel, max_throttle, bound;
+    /* model 0: differential drive (FG_eval).  model 1: kinematic bicycle (no reference
+     * implementation in the fork): the control w is the steering angle
+     * delta and the heading rows read th1 - (th0 + v0 delta0 / lf dt),
+     * eth1 - (eth0 + v0 delta0 / lf dt) (driving_state.cpp:247's commented
+     * theta_act = v * steering * dt / Lf). */
+    int model;
+    double lf;
 } ora_mpc_params;
 
 int ora_mpc_nx(int steps);  /* 6N + 2(N-1) */

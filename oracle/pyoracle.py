@@ -22,6 +22,7 @@ class MpcParams(C.Structure):
         ("w_cte", C.c_double), ("w_etheta", C.c_double), ("w_v", C.c_double), ("w_angvel", C.c_double),
         ("w_accel", C.c_double), ("w_angvel_d", C.c_double), ("w_accel_d", C.c_double),
         ("max_angvel", C.c_double), ("max_throttle", C.c_double), ("bound", C.c_double),
+        ("model", C.c_int), ("lf", C.c_double),
     ]
 
 
@@ -92,6 +93,8 @@ def params_from_dict(d: dict) -> MpcParams:
     p.max_angvel = d["ANGVEL"]
     p.max_throttle = d["MAXTHR"]
     p.bound = d["BOUND"]
+    p.model = int(d.get("MODEL", 0))  # extension keys (not in the reference map): kinematic bicycle
+    p.lf = float(d.get("LF", 0.5))
     return p
 
 

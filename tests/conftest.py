@@ -55,6 +55,17 @@ def variants_golden():
 
 
 @pytest.fixture(scope="session")
+def bicycle_golden():
+    """Kinematic-bicycle variant (tests/golden/bicycle_N25.npz): params dict includes MODEL/LF."""
+    g = load_npz("bicycle_N25.npz")
+    P = params_from_array(g["params"])
+    P["MODEL"] = int(g["model"])
+    P["LF"] = float(g["lf"])
+    g["P"] = P
+    return g
+
+
+@pytest.fixture(scope="session")
 def libmpcg():
     from mpc_ros_amd import build, _lib
 

@@ -14,6 +14,11 @@ Fixtures (data only -- inputs and expected outputs):
   variants.npz       other parameter sets (class defaults, W_DA = 0, rate penalty on w,
                      N = 40, N = 3, small BOUND with active state bounds)
   preprocess.npz     findBestPath inputs (poses, waypoints) and the oracle's outputs
+  bicycle_N25.npz    the kinematic-bicycle variant (BASELINE configs[4]; no reference
+                     implementation exists, so this pins the build's own restatement):
+                     64 infinity-set problems, N = 25, MODEL = 1, LF = 0.5, ANGVEL = 0.5
+
+    python tests/golden/make_goldens.py [set ...]     (default: all sets)
 """
 from __future__ import annotations
 
@@ -124,6 +129,18 @@ def preprocess():
                         coeffs=cf)
 
 
+BICYCLE = dict(PLUGIN, STEPS=25, MODEL=1, LF=0.5, ANGVEL=0.5)
+
+
+def bicycle():
+    st, cf = infinity.make_problems(np.arange(7000, 7064))
+    d = solve_set(BICYCLE, st, cf)
+    d["model"] = np.int32(1)
+    d["lf"] = np.float64(BICYCLE["LF"])
+    np.savez_compressed(os.path.join(HERE, "bicycle_N25.npz"), **d)
+    print("bicycle_N25 status:", np.unique(d["status"], return_counts=True), "iters mean", d["iters"].mean())
+
+
 def hs071():
     with open(os.path.join(HERE, "hs071.json"), "w") as f:
         json.dump({"source": "assets/document/example/CppAD_Ipopt.cpp:146-150",
@@ -133,11 +150,19 @@ def hs071():
 
 if __name__ == "__main__":
     O.build(force=True)
-    hs071()
-    preprocess()
-    infinity_set()
-    variants()
-    if os.path.isdir("/root/reference/mpc_ros/include/cppad"):
-        cppad_derivs()
-    else:
-        print("reference tree absent: cppad_derivs.npz not regenerated")
+    sets = set(sys.argv[1:]) or {"hs071", "preprocess", "infinity", "variants", "bicycle", "cppad"}
+    if "hs071" in sets:
+        hs071()
+    if "preprocess" in sets:
+        preprocess()
+    if "infinity" in sets:
+        infinity_set()
+    if "variants" in sets:
+        variants()
+    if "bicycle" in sets:
+        bicycle()
+    if "cppad" in sets:
+        if os.path.isdir("/root/reference/mpc_ros/include/cppad"):
+            cppad_derivs()
+        else:
+            print("reference tree absent: cppad_derivs.npz not regenerated")

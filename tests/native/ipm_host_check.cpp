@@ -32,6 +32,11 @@ int main() {
     P.bound_relax_factor = 1e-8;
     P.mu_init = 0.1;
     P.filter_cap = 64;
+    P.model = 0;
+    P.lf = 0.5;
+    int model;
+    if (std::scanf("%d %lf", &model, &P.lf) != 2) return 1;
+    if (model != 0) return 2;  // the lane solver implements the differential drive only
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     mpcg::IpmLayout L{P.N};

@@ -84,6 +84,9 @@ int main() {
     P.bound_relax_factor = 1e-8;
     P.mu_init = 0.1;
     P.filter_cap = 64;
+    P.model = 0;
+    P.lf = 0.5;
+    if (std::scanf("%d %lf", &P.model, &P.lf) != 2) return 1;
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     const mpcg::WideLayout L{P.N, P.filter_cap};
@@ -100,17 +103,25 @@ int main() {
         for (int t = 0; t < 64; ++t) {
             th.emplace_back([&, t]() {
                 HostWave wv{&sh, t, sh.lds.data()};
-                mpcg::WideSolver<HostWave> S(P, pr, wv);
-                S.solve();
-                const double o = S.objective_out();
-                if (t == 0) {
-                    status = S.status;
-                    iters = S.iter;
-                    obj = o;
-                    u0 = S.x_ctrl(0, 0);
-                    u1 = S.x_ctrl(1, 0);
-                    for (int s = 0; s < 3; ++s)
-                        for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
+                auto run = [&](auto& S) {
+                    S.solve();
+                    const double o = S.objective_out();
+                    if (t == 0) {
+                        status = S.status;
+                        iters = S.iter;
+                        obj = o;
+                        u0 = S.x_ctrl(0, 0);
+                        u1 = S.x_ctrl(1, 0);
+                        for (int s = 0; s < 3; ++s)
+                            for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
+                    }
+                };
+                if (P.model == 1) {
+                    mpcg::WideSolver<HostWave, 1> S(P, pr, wv);
+                    run(S);
+                } else {
+                    mpcg::WideSolver<HostWave, 0> S(P, pr, wv);
+                    run(S);
                 }
             });
         }

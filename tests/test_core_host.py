@@ -28,7 +28,8 @@ def run_harness(exe, P, state, coeffs, tol=1e-8, max_iter=3000):
     N = int(P["STEPS"])
     hdr = (f"{N} {P['DT']!r} {P['REF_CTE']!r} {P['REF_ETHETA']!r} {P['REF_V']!r} {P['W_CTE']!r} {P['W_EPSI']!r} "
            f"{P['W_V']!r} {P['W_ANGVEL']!r} {P['W_A']!r} {P['W_DANGVEL']!r} {P['W_DA']!r} {P['ANGVEL']!r} "
-           f"{P['MAXTHR']!r} {P['BOUND']!r} {tol!r} {max_iter}\n{len(state)}\n")
+           f"{P['MAXTHR']!r} {P['BOUND']!r} {tol!r} {max_iter}\n{int(P.get('MODEL', 0))} {float(P.get('LF', 0.5))!r}\n"
+           f"{len(state)}\n")
     body = "\n".join(" ".join(repr(float(v)) for v in np.concatenate([state[b], coeffs[b]]))
                      for b in range(len(state)))
     out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True).stdout
@@ -85,4 +86,13 @@ def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
     n = 6
     sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
+    compare(r, sub, atol=1e-9)
+
+
+def test_wide_core_bicycle_matches_oracle(wide_harness, bicycle_golden):
+    """Kinematic-bicycle variant (N = 25) through the wavefront solver."""
+    g = bicycle_golden
+    n = 12
+    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)

@@ -189,3 +189,19 @@ def test_strategies_agree_at_full_size(torch_cuda):
     assert np.mean(a["iters"] == b["iters"]) > 0.99
     same = a["status"] == b["status"]
     assert np.abs(a["u0"][same] - b["u0"][same]).max() < 1e-6
+
+
+def test_bicycle_matches_oracle(torch_cuda, bicycle_golden):
+    """BASELINE configs[4]'s model (kinematic bicycle, N = 25) on the wavefront kernel."""
+    g = bicycle_golden
+    s = solver_for(g["P"])
+    assert s.strategy == "wave"
+    check_against(s.solve(g["state"], g["coeffs"]), g)
+
+
+def test_bicycle_refused_by_lane_strategy(torch_cuda, bicycle_golden):
+    from mpc_ros_amd._lib import MpcgError
+
+    g = bicycle_golden
+    with pytest.raises(MpcgError):
+        solver_for(g["P"], strategy="lane").solve(g["state"][:4], g["coeffs"][:4])

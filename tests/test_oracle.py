@@ -114,3 +114,52 @@ def test_preprocess_restatement(oracle):
         np.testing.assert_allclose(cf, z["coeffs"][b], atol=1e-13)
     rc, _, _ = oracle.find_best_path(0, 0, 0, 0, 0, 0, 0.1, np.zeros((0, 2)), True)
     assert rc == -1  # empty plan (driving_state.cpp:182-185)
+
+
+# --------------------------------------------------------- kinematic bicycle (model 1)
+# No reference implementation exists: the NLP is pinned by its own
+# derivative consistency (analytic vs central differences of fg) and by the KKT
+# certificate of the committed solutions; parity unpinned against Ipopt.
+def test_bicycle_derivatives_match_finite_differences(oracle, bicycle_golden):
+    P = dict(bicycle_golden["P"], STEPS=6)
+    N = 6
+    nx, ng = 8 * N - 2, 6 * N
+    rng = np.random.default_rng(3)
+    c = bicycle_golden["coeffs"][0]
+    x = rng.normal(scale=0.5, size=nx)
+    lam = rng.normal(scale=5.0, size=ng)
+    gf, J, H = oracle.mpc_derivs(P, c, x, 0.7, lam)
+    h = 1e-6
+    Jfd = np.zeros((1 + ng, nx))
+    for i in range(nx):
+        e = np.zeros(nx)
+        e[i] = h
+        Jfd[:, i] = (oracle.mpc_fg(P, c, x + e) - oracle.mpc_fg(P, c, x - e)) / (2 * h)
+    np.testing.assert_allclose(gf, Jfd[0], rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(J, Jfd[1:], rtol=1e-6, atol=1e-6)
+    # Hessian of the Lagrangian by differences of the analytic gradients
+    def grad_l(xx):
+        g0, JJ, _ = oracle.mpc_derivs(P, c, xx, 0.7, lam)
+        return 0.7 * g0 + JJ.T @ lam
+    Hfd = np.zeros((nx, nx))
+    for i in range(nx):
+        e = np.zeros(nx)
+        e[i] = h
+        Hfd[:, i] = (grad_l(x + e) - grad_l(x - e)) / (2 * h)
+    np.testing.assert_allclose(H, Hfd, rtol=1e-5, atol=1e-4)
+
+
+def test_bicycle_fixtures_reproduce_and_certify(oracle, bicycle_golden):
+    g = bicycle_golden
+    P = g["P"]
+    sel = np.arange(0, 64, 4)
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ipm_opts(tol=1e-8))
+    np.testing.assert_array_equal(r["status"], g["status"][sel])
+    np.testing.assert_array_equal(r["iters"], g["iters"][sel])
+    np.testing.assert_allclose(r["u0"], g["u0"][sel], rtol=0, atol=1e-12)
+    for b in sel[:6]:
+        if g["status"][b] != 1:
+            continue
+        full = oracle.mpc_solve(P, g["state"][b], g["coeffs"][b], opts=oracle.ipm_opts(tol=1e-8), full=True)
+        res = oracle.mpc_kkt_residual(P, g["state"][b], g["coeffs"][b], full["x"])
+        assert res["primal"] < 1e-8 and res["bound"] <= 1e-12
