@@ -78,6 +78,8 @@ struct DevWaveBase {
     __device__ __forceinline__ double dn1(double v) const { return dpp<0x130>(v); }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
     __device__ __forceinline__ int uni(int v) const { return __builtin_amdgcn_readfirstlane(v); }
+    // scheduling barrier: instructions are not moved across it (no wait is inserted)
+    __device__ __forceinline__ void sched_fence() const { __builtin_amdgcn_sched_barrier(0); }
     __device__ __forceinline__ double uni_d(double v) const {
         return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
                                 __builtin_amdgcn_readfirstlane(__double2loint(v)));

@@ -594,12 +594,24 @@ struct WideSolver {
         bool bad = false;  // a stage's reduced Hessian not positive definite
         for (int k = N - 2; k >= 0; --k) {
             const int sb = L.ST(k);
-            // row i of P' (16-byte reads of the scratch the previous stage wrote)
-            T pr_[8], g[8];
+            // row i of P' (16-byte reads of the scratch the previous stage wrote) and all
+            // P-independent stage data, issued together before anything waits on them
+            T pr_[8], g[8], c[8];
             wv.sync();
             ldv<8>(sp + 8 * i, pr_);
 #pragma unroll
             for (int q = 0; q < 8; ++q) g[q] = ld(sb + go[q]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c[q] = ld(sb + ao[q]);
+            T qd6, qd7, qv6, qv7;
+            ld2(sb + W_::SQD + 6, qd6, qd7);
+            ld2(sb + W_::SQV + 6, qv6, qv7);
+            const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
+            const T qh1 = ld(sb + q1), qh2 = ld(sb + q2);
+            const T qvi = ld(sb + qv);
+            const T hv0j = model == 1 ? ld(sb + hvj) : (T)0, hv0i = model == 1 ? ld(sb + hvi) : (T)0;
+            const T tw = model == 1 ? ld(sb + W_::STW) : dt;
+            wv.sched_fence();  // (nothing above consumes a load: no wait here)
             // M = P' G, entry (i, j) per lane; column 7 adds p' (h = P' d + p')
             T m0 = (j == 7) ? pvi : (T)0, m1 = 0;
 #pragma unroll
@@ -617,17 +629,7 @@ struct WideSolver {
             const T m25 = ld(sm + 42), m55 = ld(sm + 45), m65 = ld(sm + 46);
             const T m26 = ld(sm + 50), m36 = ld(sm + 51), m56 = ld(sm + 53), m66 = ld(sm + 54), m76 = ld(sm + 55);
             const T mi2 = ld(mi + 2), mi3 = ld(mi + 3), mi5 = ld(mi + 5), mi6 = ld(mi + 6), mi7 = ld(mi + 7);
-            T c[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) c[q] = ld(sb + ao[q]);
-            T qd6, qd7, qv6, qv7;
-            ld2(sb + W_::SQD + 6, qd6, qd7);
-            ld2(sb + W_::SQV + 6, qv6, qv7);
-            const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
-            const T hv0j = model == 1 ? ld(sb + hvj) : (T)0, hv0i = model == 1 ? ld(sb + hvi) : (T)0;
-            const T tw = model == 1 ? ld(sb + W_::STW) : dt;
-            const T qh = ld(sb + q1) + ld(sb + q2);
-            const T qvi = ld(sb + qv);
+
             // R_tilde = R + B^T P' B, r_tilde = r + B^T h, S_tilde = B^T P' A (+ rate coupling)
             const T Rt00 = qd6 + (tw * (m25 + m55) + m65);
             const T Rt01 = tw * (m26 + m56) + m66;
@@ -655,6 +657,7 @@ struct WideSolver {
                 h0 += c[q] * m7[q];
                 h1 += c[q + 1] * m7[q + 1];
             }
+            const T qh = qh1 + qh2;
             Pij = qh + (hj ? a0 + a1 : (T)0) + s0i * K0 + s1i * K1;
             pvi = qvi + (h0 + h1) + s0i * kf0 + s1i * kf1;
             st(sp + t, Pij);

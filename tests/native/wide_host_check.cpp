@@ -51,6 +51,7 @@ struct HostWave {
     }
     int uni(int v) const { return v; }
     void mark(int) const {}
+    void sched_fence() const {}
     void ld2(int i, double& a, double& b) const {
         a = lds[i];
         b = lds[i + 1];
