@@ -188,7 +188,8 @@ def main():
             got = fl * count / (kern * 1e-3) / 1e12
             valu = {"achieved": got, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": got / FP64_VALU_PEAK_TFLOPS, "flops_per_solve": fl,
-                    "source": f"profiles/{prof}.json (SQ_INSTS_VALU_FLOPS_FP64)"}
+                    "source": f"profiles/{prof}.json (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes: physical FP64 "
+                              f"lane-FLOPs, replicated and idle lanes included)"}
         line = {
             "metric": "NMPC solves/sec (whole node), N=20 diff-drive, at 1/2/4/8 MI355X",
             "value": value,

@@ -25,7 +25,12 @@ import os
 def load(root: str, kernel: str = "k_solve_wide"):
     vals = collections.defaultdict(list)
     times = []
-    for f in sorted(glob.glob(os.path.join(root, "*", "*", "*_counter_collection.csv"))):
+    files = {}
+    for f in glob.glob(os.path.join(root, "*", "*", "*_counter_collection.csv")):
+        d = os.path.dirname(os.path.dirname(f))  # one pass per directory: its newest file
+        if d not in files or os.path.getmtime(f) > os.path.getmtime(files[d]):
+            files[d] = f
+    for f in sorted(files.values()):
         per = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
             if kernel not in r.get("Kernel_Name", ""):
@@ -64,8 +69,15 @@ def main():
     if "GRBM_GUI_ACTIVE" in c and t:
         out["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
     if "SQ_INSTS_VALU_FLOPS_FP64" in c:
-        out["fp64_flops_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"] + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
-        out["fp64_flops_per_solve"] = out["fp64_flops_per_launch"] / B
+        # the FLOPS counters count per wave-instruction (ADD + MUL + 2 FMA reproduces them,
+        # measured): physical lane FLOPs = x 64 lanes (idle and replicated lanes included)
+        wave = c["SQ_INSTS_VALU_FLOPS_FP64"] + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
+        out["fp64_wave_flops_per_solve"] = wave / B
+        out["fp64_flops_per_launch"] = 64 * wave
+        out["fp64_flops_per_solve"] = 64 * wave / B
+        for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64"):
+            if k in c:
+                out[k.lower() + "_per_solve"] = c[k] / B
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
