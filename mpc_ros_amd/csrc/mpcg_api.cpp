@@ -39,6 +39,9 @@ struct mpcg_handle {
     // mpcg_track_device intermediates: state [B][6] | coeffs [B][4] | u0 [B][2]
     double* d_trk = nullptr;
     size_t trk_bytes = 0;
+    // solve-order buffers of the wave strategy (keys, indices, sort scratch)
+    void* d_sched = nullptr;
+    size_t sched_bytes = 0;
 };
 
 extern "C" {
@@ -215,6 +218,7 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->ws) hipFree(h->ws);
     if (h->d_io) hipFree(h->d_io);
     if (h->d_trk) hipFree(h->d_trk);
+    if (h->d_sched) hipFree(h->d_sched);
     if (h->drv.d_active) hipFree(h->drv.d_active);
     if (h->drv.h_active) hipHostFree(h->drv.h_active);
     for (hipEvent_t ev : h->drv.ev)
@@ -253,9 +257,31 @@ static int ensure_ws(mpcg_handle* h, int64_t B) {
     return 0;
 }
 
+// solve-order buffers of the wave strategy (batches beyond the resident wavefronts)
+static const int64_t kOrderMinBatch = 2048;
+
+static int ensure_sched(mpcg_handle* h, int64_t B) {
+    const size_t need = mpcg::wide_sched_bytes(B);
+    if (need <= h->sched_bytes) return 0;
+    hipSetDevice(h->device);
+    if (h->d_sched) {
+        hipDeviceSynchronize();  // may be in use on any stream
+        hipFree(h->d_sched);
+        h->d_sched = nullptr;
+        h->sched_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&h->d_sched, need);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(schedule buffers)");
+    h->sched_bytes = need;
+    return 0;
+}
+
+static int resolve_strategy(const mpcg_handle* h);
+
 int mpcg_reserve(mpcg_handle* h, int64_t B) {
     if (!h) return fail(-1, "null handle");
     if (B < 0) return fail(-1, "negative batch");
+    if (resolve_strategy(h) == MPCG_STRATEGY_WAVE) return B > kOrderMinBatch ? ensure_sched(h, B) : 0;
     return ensure_ws(h, B);
 }
 
@@ -296,7 +322,18 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
     if (strat == MPCG_STRATEGY_WAVE) {
         if (P.N > 64 || mpcg::wide_lds_bytes(P) > kWideLdsMax)
             return fail(-1, "strategy WAVE needs steps <= 64 and the problem state within 64 KiB of LDS");
-        e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, s);
+        // batches larger than the resident wavefronts (8 per CU) are solved in
+        // expected-longest-first order (launch_wide_order)
+        const int32_t* order = nullptr;
+        if (B > kOrderMinBatch) {
+            rc = ensure_sched(h, B);
+            if (rc) return rc;
+            int32_t* ord = nullptr;
+            e = mpcg::launch_wide_order(B, d_coeffs, h->d_sched, h->sched_bytes, &ord, s);
+            if (e != hipSuccess) return hip_fail(e, "solve-order sort");
+            order = ord;
+        }
+        e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, s);
         if (e != hipSuccess) return hip_fail(e, "wide solve launch");
         return 0;
     }

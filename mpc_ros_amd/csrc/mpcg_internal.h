@@ -27,7 +27,13 @@ hipError_t launch_ipm_solve(const IpmParams& P, int64_t B, const double* state, 
 // One problem per wavefront (mpcg_wide.hip): LDS bytes per problem, launch.
 size_t wide_lds_bytes(const IpmParams& P);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
-                             double* traj, int32_t* status, double* obj, int32_t* iters, hipStream_t stream);
+                             double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
+                             hipStream_t stream);
+// Solve order (expected-longest first): device buffer bytes for B problems, and the
+// launch that writes the workgroup -> problem map into `buf` (returned in *order).
+size_t wide_sched_bytes(int64_t B);
+hipError_t launch_wide_order(int64_t B, const double* coeffs, void* buf, size_t bytes, int32_t** order,
+                             hipStream_t stream);
 
 // findBestPath preprocessing and post-processing (mpcg_track.hip).
 hipError_t launch_find_best_path(int64_t B, int M, double dt, int delay_mode, const double* pose, const double* vel,

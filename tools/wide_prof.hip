@@ -11,6 +11,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "../mpc_ros_amd/csrc/wave_dev.h"
@@ -34,7 +35,8 @@ struct ProfWave : DevWaveBase {
 #define WPE 1
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_prof(IpmParams P, int64_t B, const double* state, const double* coeffs,
-                                             unsigned long long* acc, int* iters, int* status) {
+                                             unsigned long long* acc, int* iters, int* status,
+                                             unsigned long long* times) {
     const int64_t p = blockIdx.x;
     if (p >= B) return;
     IpmProblem<double> pr;
@@ -45,9 +47,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     wv.acc = acc + p * (NPH + 1);
     wv.last = (unsigned long long)clock64();
     const unsigned long long t0 = wv.last;
+    const unsigned long long r0 = wall_clock64();
     WideSolver<ProfWave> S(P, pr, wv);
     S.solve();
     if (threadIdx.x == 0) {
+        times[2 * p] = r0;
+        times[2 * p + 1] = wall_clock64();
         acc[p * (NPH + 1) + NPH] = clock64() - t0;
         iters[p] = S.iter;
         status[p] = S.status;
@@ -89,6 +94,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dacc, B * W * 8));
     CK(hipMalloc(&dit, B * 4));
     CK(hipMalloc(&dss, B * 4));
+    unsigned long long* dtm;
+    CK(hipMalloc(&dtm, B * 16));
     CK(hipMemcpy(dst, st.data(), B * 6 * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dcf, cf.data(), B * 4 * 8, hipMemcpyHostToDevice));
     CK(hipMemset(dacc, 0, B * W * 8));
@@ -98,7 +105,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss);
+    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss, dtm);
     CK(hipGetLastError());
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
@@ -119,5 +126,19 @@ int main(int argc, char** argv) {
         std::printf("  %-10s %10.0f cyc/solve %8.0f cyc/iter  %5.1f%%\n", mpcg::kPhase[j], sum[j] / B, sum[j] / iters,
                     100.0 * sum[j] / sum[mpcg::NPH]);
     std::printf("  %-10s %10.0f cyc/solve %8.0f cyc/iter\n", "total", sum[mpcg::NPH] / B, sum[mpcg::NPH] / iters);
+    // dispatch timeline (wall_clock64 ticks, 100 MHz): when problems start and end
+    std::vector<unsigned long long> tm(2 * B);
+    CK(hipMemcpy(tm.data(), dtm, B * 16, hipMemcpyDeviceToHost));
+    unsigned long long tmin = ~0ull, tmax = 0;
+    std::vector<double> ends(B);
+    for (int64_t p = 0; p < B; ++p) { tmin = std::min(tmin, tm[2 * p]); tmax = std::max(tmax, tm[2 * p + 1]); }
+    for (int64_t p = 0; p < B; ++p) ends[p] = (tm[2 * p + 1] - tmin) * 1e-5;  // ms at 100 MHz
+    std::vector<double> srt(ends);
+    std::sort(srt.begin(), srt.end());
+    std::printf("timeline ms: first end %.3f, 50%% %.3f, 90%% %.3f, 99%% %.3f, 99.9%% %.3f, last %.3f\n", srt[0],
+                srt[B / 2], srt[(B * 9) / 10], srt[(B * 99) / 100], srt[(B * 999) / 1000], srt[B - 1]);
+    int64_t pl = 0;
+    for (int64_t p = 0; p < B; ++p) if (ends[p] == srt[B - 1]) pl = p;
+    std::printf("last problem %lld: start %.3f ms, iters %d\n", (long long)pl, (tm[2 * pl] - tmin) * 1e-5, it[pl]);
     return 0;
 }
