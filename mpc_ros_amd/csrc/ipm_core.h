@@ -1027,7 +1027,9 @@ struct IpmSolver {
         const T dual_uns = dual_inf / sf;
         set_sc(SC_KKT, tmax(dual_uns, tmax(prim_uns, compl0)));
         int st = 0;
-        if (!isfinite((double)E0))
+        // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
+        // drop a NaN; the sums do not)
+        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval))
             st = IPM_INVALID_NUMBER;
         else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4)
             st = IPM_SUCCESS;

@@ -978,7 +978,9 @@ struct WideSolver {
         const T dual_uns = dual_inf / sf;
         kkt = tmax(dual_uns, tmax(prim_uns, compl0));
         int s = 0;
-        if (!isfinite((double)E0))
+        // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
+        // drop a NaN; the sums do not)
+        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval))
             s = IPM_INVALID_NUMBER;
         else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4)
             s = IPM_SUCCESS;

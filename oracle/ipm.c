@@ -300,7 +300,13 @@ int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out
         if (opts.print_level > 0)
             fprintf(stderr, "iter %3d mu %.2e E0 %.3e dual %.3e prim %.3e compl %.3e f %.10e\n", iter,
                     mu, E0, dual_inf, prim_inf, compl0, eval_f(&C, w) / C.obj_scale);
-        if (!isfinite(E0)) { status = ORA_INVALID_NUMBER_DETECTED; break; }
+        /* Ipopt's finiteness test of f and g at an evaluated point (OrigIpoptNLP, Ipopt
+         * 3.12.8, not vendored in the reference) -> INVALID_NUMBER_DETECTED: amax()
+         * drops a NaN, the l1 norm and f do not */
+        if (!isfinite(E0) || !isfinite(l1(m, cv)) || !isfinite(eval_f(&C, w))) {
+            status = ORA_INVALID_NUMBER_DETECTED;
+            break;
+        }
         if (E0 <= opts.tol && dual_unscaled <= 1.0 && prim_unscaled <= 1e-4 && compl0 <= 1e-4) {
             status = ORA_SUCCESS;
             break;

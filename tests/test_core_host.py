@@ -96,3 +96,52 @@ def test_wide_core_bicycle_matches_oracle(wide_harness, bicycle_golden):
     sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
     r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
+
+
+def _oracle_run(oracle, P, state, coeffs):
+    return oracle.mpc_solve_batch(P, state, coeffs, opts=oracle.ipm_opts(tol=1e-8), nthreads=4)
+
+
+def test_wide_core_full_width_N64(wide_harness, oracle):
+    """STEPS = 64, the widest horizon the wavefront strategy takes (one stage per
+    lane, every lane active), against the oracle on benchmark scenarios."""
+    from mpc_ros_amd import infinity, params
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=64)
+    sc = infinity.draw_scenarios(np.arange(200, 206))
+    px, py, yaw, plan = infinity.scenario_poses(sc)
+    st, cf = infinity.find_best_path(px, py, yaw, sc["v"], sc["w_prev"], sc["a_prev"], P["DT"], plan, True)
+    g = _oracle_run(oracle, P, st, cf)
+    r = run_harness(wide_harness, P, st, cf)
+    compare(r, g, atol=1e-9)
+
+
+def nonfinite_inputs():
+    """NaN / inf in the state or the path polynomial, and a huge finite state."""
+    st = np.tile(np.array([0.05, 0.0, 0.02, 0.4, 0.1, 0.05]), (6, 1))
+    cf = np.tile(np.array([0.1, 0.02, -0.01, 0.001]), (6, 1))
+    st[0, 3] = np.nan
+    cf[1, 2] = np.inf
+    st[2, 0] = 1e300
+    cf[3, 0] = -np.inf
+    st[4, 5] = np.nan
+    return st, cf
+
+
+def test_nonfinite_inputs_stop_with_invalid_number(harness, wide_harness, oracle):
+    """A non-finite f or g at the starting point ends the solve before the first
+    iteration with Ipopt's INVALID_NUMBER_DETECTED (11) -- no hang, no iterations --
+    in the oracle and in both device cores; finite rows are unaffected."""
+    from mpc_ros_amd import params
+
+    P = params.PLUGIN_DEFAULTS
+    st, cf = nonfinite_inputs()
+    g = _oracle_run(oracle, P, st, cf)
+    np.testing.assert_array_equal(g["status"][[0, 1, 3, 4]], 11)
+    np.testing.assert_array_equal(g["iters"][[0, 1, 3, 4]], 0)
+    assert g["status"][5] == 1
+    for exe in (harness, wide_harness):
+        r = run_harness(exe, P, st, cf)
+        np.testing.assert_array_equal(r["status"], g["status"])
+        np.testing.assert_array_equal(r["iters"], g["iters"])
+        np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=1e-9)

@@ -205,3 +205,36 @@ def test_bicycle_refused_by_lane_strategy(torch_cuda, bicycle_golden):
     g = bicycle_golden
     with pytest.raises(MpcgError):
         solver_for(g["P"], strategy="lane").solve(g["state"][:4], g["coeffs"][:4])
+
+
+@pytest.mark.parametrize("strategy", STRATS)
+def test_full_width_N64(torch_cuda, oracle, strategy):
+    """STEPS = 64: every lane of the wavefront carries a stage (the widest the wave
+    strategy takes); the lane strategy on the same problems."""
+    from mpc_ros_amd import infinity, params
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=64)
+    sc = infinity.draw_scenarios(np.arange(300, 316))
+    px, py, yaw, plan = infinity.scenario_poses(sc)
+    st, cf = infinity.find_best_path(px, py, yaw, sc["v"], sc["w_prev"], sc["a_prev"], P["DT"], plan, True)
+    g = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ipm_opts(tol=1e-8), nthreads=16)
+    s = solver_for(P, strategy=strategy)
+    assert s.strategy == strategy
+    check_against(s.solve(st, cf), g, min_same_iters=0.9)
+
+
+@pytest.mark.parametrize("strategy", STRATS)
+def test_nonfinite_inputs(torch_cuda, oracle, strategy):
+    """NaN / inf inputs end before the first iteration with INVALID_NUMBER_DETECTED
+    (11), as in the oracle; the other problems of the batch are unaffected."""
+    from mpc_ros_amd import params
+    from test_core_host import nonfinite_inputs
+
+    P = params.PLUGIN_DEFAULTS
+    st, cf = nonfinite_inputs()
+    g = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ipm_opts(tol=1e-8), nthreads=4)
+    r = solver_for(P, strategy=strategy).solve(st, cf)
+    np.testing.assert_array_equal(r["status"], g["status"])
+    np.testing.assert_array_equal(r["iters"], g["iters"])
+    np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=ATOL)
+    assert (g["status"] == 11).sum() == 4
