@@ -126,20 +126,30 @@ struct IpmResult {
 // fdlibm minimax kernels on [-pi/4, pi/4] (degree 13 / 14) and quadrant selection --
 // ~35 instructions, within 1-2 ulp of the correctly rounded values.  Larger
 // arguments take the library routine.
+// A double constant materialised at its use (two scalar moves) rather than hoisted
+// and kept live across the solver's loops, where it would be spilled to scratch.
+MPCG_HD double kc(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __asm__ volatile("" : "+s"(v));
+#endif
+    return v;
+}
+
 MPCG_HD void sincos_small(double a, double* s, double* c) {
-    const double inv_pio2 = 6.36619772367581382433e-01;
-    const double p1 = 1.57079632679489655800e+00, p2 = 6.12323399573676603587e-17, p3 = -1.49738490485916983e-33;
+    const double inv_pio2 = kc(6.36619772367581382433e-01);
+    const double p1 = kc(1.57079632679489655800e+00), p2 = kc(6.12323399573676603587e-17),
+                 p3 = kc(-1.49738490485916983e-33);
     const double n = rint(a * inv_pio2);
     double r = __builtin_fma(-n, p1, a);
     r = __builtin_fma(-n, p2, r);
     r = __builtin_fma(-n, p3, r);
     const double z = r * r;
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double S1 = kc(-1.66666666666666324348e-01), S2 = kc(8.33333333332248946124e-03),
+                 S3 = kc(-1.98412698298579493134e-04), S4 = kc(2.75573137070700676789e-06),
+                 S5 = kc(-2.50507602534068634195e-08), S6 = kc(1.58969099521155010221e-10);
+    const double C1 = kc(4.16666666666666019037e-02), C2 = kc(-1.38888888888741095749e-03),
+                 C3 = kc(2.48015872894767294178e-05), C4 = kc(-2.75573143513906633035e-07),
+                 C5 = kc(2.08757232129817482790e-09), C6 = kc(-1.13596475577881948265e-11);
     const double ps = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
     const double sr = __builtin_fma(r * z, __builtin_fma(z, ps, S1), r);
     const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));

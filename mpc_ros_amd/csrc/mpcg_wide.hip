@@ -1,7 +1,7 @@
 // mpc_ros_amd/csrc/mpcg_wide.hip -- one problem per wavefront (wide_core.h) on CDNA4.
 //
 // One workgroup = one wavefront = one problem; the problem's whole state lives in
-// the workgroup's LDS (WideLayout: 30 KB at N = 20, i.e. 5 problems resident per
+// the workgroup's LDS (WideLayout: 19.3 KB at N = 20, i.e. 8 problems resident per
 // CU).  Workgroups are dispatched by the hardware as CUs free up, so a slow problem
 // occupies one wavefront slot while the rest of the batch streams past it.
 #include <hip/hip_runtime.h>
@@ -105,7 +105,12 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (B <= 0) return hipSuccess;
     const size_t lds = wide_lds_bytes(P);
     const void* fn = P.model == 1 ? (const void*)k_solve_wide<1> : (const void*)k_solve_wide<0>;
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
+    hipFuncAttributes fa;
+    hipError_t e = hipFuncGetAttributes(&fa, fn);
+    if (e != hipSuccess) return e;
+    if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters};
     if (P.model == 1)

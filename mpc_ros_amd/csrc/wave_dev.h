@@ -11,7 +11,7 @@
 //                   a commutative op leaves every lane with identical bits;
 //   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
 //   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
-//   S()             the LDS base; ld2(i, a, b): 16-byte LDS load of two doubles (i even).
+//   S()             the LDS base (address 0); ld2(i, a, b): 16-byte LDS load of two doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
 #define MPCG_WAVE_DEV_H
 
@@ -25,16 +25,18 @@ namespace mpcg {
 #define MPCG_LDS
 #endif
 
-// The workgroup's dynamic LDS (one problem per workgroup).  Addressing it through the
-// symbol (a link-time constant) rather than a pointer value lets every LDS access
-// fold its offset into the instruction.
+// The workgroup's dynamic LDS (one problem per workgroup).  The solver kernels use no
+// static LDS, so the dynamic segment starts at LDS address 0 and is addressed from a
+// literal 0 base: every access is then one DS instruction on the lane's own offset
+// (through the symbol, the late-resolved base costs a v_add per per-lane address --
+// 3 % of the kernel time).  launch_wide_solve checks that the kernel has no static LDS.
 extern __shared__ double mpcg_dyn_lds[];
 
 struct DevWaveBase {
     typedef MPCG_LDS double ldsT;
     typedef MPCG_LDS double2 ldsT2;
     int t;
-    __device__ __forceinline__ static ldsT* S() { return (ldsT*)mpcg_dyn_lds; }
+    __device__ __forceinline__ static ldsT* S() { return (ldsT*)(__SIZE_TYPE__)0; }
 
     __device__ __forceinline__ void sync() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -63,11 +63,16 @@ struct WideLayout {
     MPCG_HD int YP(int k) const { return 40 * N + 8 * k; }
     MPCG_HD int KR(int k) const { return 48 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
     MPCG_HD int ST(int k) const { return 64 * N + SS * k; }
-    // scratch of the Riccati sweep: M^T (M[r][c] at 8 c + r), then P row-major
+    // scratch of the Riccati sweep: G^T of the stage, then M^T (M[r][c] at MS c + r) in
+    // the same 8 columns, MS = 10 doubles apart (16-byte column reads of different
+    // columns fall in different LDS banks); then P row-major
+    static constexpr int MS = 10;
     MPCG_HD int SCR() const { return (64 + SS) * N; }
-    MPCG_HD int RSC() const { return (64 + SS) * N + 128; }  // row scales: ra[6] rb[6] 1.0 (+pad)
-    MPCG_HD int FI() const { return (64 + SS) * N + 144; }
-    MPCG_HD int total() const { return (64 + SS) * N + 144 + 2 * cap; }
+    MPCG_HD int PSC() const { return (64 + SS) * N + 8 * MS; }
+    MPCG_HD int RSC() const { return (64 + SS) * N + 8 * MS + 64; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int ZB() const { return RSC() + 16; }                    // 8 zeros (an absent column)
+    MPCG_HD int FI() const { return RSC() + 24; }
+    MPCG_HD int total() const { return FI() + 2 * cap; }
 };
 
 // MODEL: 0 differential drive (FG_eval), 1 kinematic bicycle -- a template parameter
@@ -262,6 +267,7 @@ struct WideSolver {
             }
             st(L.RSC() + 12, 1);
         }
+        if (t < 8) st(L.ZB() + t, 0);
     }
     MPCG_HD T push(T v, T lo, T hi) const {
         const T pl = tmin((T)0.01 * tmax((T)1, (T)fabs(lo)), (T)0.01 * (hi - lo));
@@ -557,17 +563,17 @@ struct WideSolver {
         typedef WideLayout W_;
         const int i = t >> 3, j = t & 7;
         const int si = aslot(i), sj = aslot(j);
-        const int sm = L.SCR(), sp = L.SCR() + 64;
-        // per-lane stage-table offsets: G column j, A_hat column i
-        int go[8], ao[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            go[q] = goff(j, q);
-            ao[q] = goff(si, q);
-        }
-        // columns sj and si of M (clamped, masked by hj / hi) and the rate-coupling entries of S_tilde
+        constexpr int MS = WideLayout::MS;
+        const int sm = L.SCR(), sp = L.PSC();
+        // The stage's G is staged densely (transposed) in the M scratch by the previous
+        // stage, each lane copying its entry G[j][i] out of the stage table: a lane then
+        // reads G column j and A_hat column i (= G column si) with 16-byte loads off one
+        // address each.  An absent A_hat column (si, sj < 0) reads the zero block, so
+        // its products vanish without masking.
         const bool hj = sj >= 0, hi = si >= 0;
-        const int mj = sm + 8 * (hj ? sj : 0), mi = sm + 8 * (hi ? si : 0);
+        const int gj = sm + MS * j, mi = hi ? sm + MS * si : L.ZB(), mj = hj ? sm + MS * sj : L.ZB();
+        const int gsrc = goff(i, j);
+        // the rate-coupling entries of S_tilde
         const int c0j = j == 6 ? W_::SCC : W_::SZERO, c1j = j == 7 ? W_::SCC + 1 : W_::SZERO;
         const int c0i = i == 6 ? W_::SCC : W_::SZERO, c1i = i == 7 ? W_::SCC + 1 : W_::SZERO;
         // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
@@ -590,6 +596,7 @@ struct WideSolver {
             Pij = ld(sb + q1);
             pvi = ld(sb + qv);
             st(sp + t, Pij);
+            if (N >= 2) st(sm + MS * i + j, ld(L.ST(N - 2) + gsrc));
         }
         bool bad = false;  // a stage's reduced Hessian not positive definite
         for (int k = N - 2; k >= 0; --k) {
@@ -599,17 +606,20 @@ struct WideSolver {
             T pr_[8], g[8], c[8];
             wv.sync();
             ldv<8>(sp + 8 * i, pr_);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) g[q] = ld(sb + go[q]);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) c[q] = ld(sb + ao[q]);
+            ldv<8>(gj, g);
+            ldv<8>(mi, c);
+            const T gnext = ld(L.ST(k > 0 ? k - 1 : 0) + gsrc);  // next stage's G entry
             T qd6, qd7, qv6, qv7;
             ld2(sb + W_::SQD + 6, qd6, qd7);
             ld2(sb + W_::SQV + 6, qv6, qv7);
             const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
             const T qh1 = ld(sb + q1), qh2 = ld(sb + q2);
             const T qvi = ld(sb + qv);
-            const T hv0j = model == 1 ? ld(sb + hvj) : (T)0, hv0i = model == 1 ? ld(sb + hvi) : (T)0;
+            T hv0j = 0, hv0i = 0;
+            if constexpr (MODEL == 1) {
+                hv0j = ld(sb + hvj);
+                hv0i = ld(sb + hvi);
+            }
             const T tw = model == 1 ? ld(sb + W_::STW) : dt;
             wv.sched_fence();  // (nothing above consumes a load: no wait here)
             // M = P' G, entry (i, j) per lane; column 7 adds p' (h = P' d + p')
@@ -620,14 +630,15 @@ struct WideSolver {
                 m1 += pr_[q + 1] * g[q + 1];
             }
             wv.sync();  // the previous stage's reads of M are done
-            st(sm + 8 * j + i, m0 + m1);
+            st(sm + MS * j + i, m0 + m1);
             wv.sync();
             // columns of M: sj and 7 (all rows), B_hat rows (2,3,5,6,7) of 5, 6 and si
             T mc[8], m7[8];
             ldv<8>(mj, mc);
-            ldv<8>(sm + 56, m7);
-            const T m25 = ld(sm + 42), m55 = ld(sm + 45), m65 = ld(sm + 46);
-            const T m26 = ld(sm + 50), m36 = ld(sm + 51), m56 = ld(sm + 53), m66 = ld(sm + 54), m76 = ld(sm + 55);
+            ldv<8>(sm + MS * 7, m7);
+            const T m25 = ld(sm + MS * 5 + 2), m55 = ld(sm + MS * 5 + 5), m65 = ld(sm + MS * 5 + 6);
+            const T m26 = ld(sm + MS * 6 + 2), m36 = ld(sm + MS * 6 + 3), m56 = ld(sm + MS * 6 + 5),
+                    m66 = ld(sm + MS * 6 + 6), m76 = ld(sm + MS * 6 + 7);
             const T mi2 = ld(mi + 2), mi3 = ld(mi + 3), mi5 = ld(mi + 5), mi6 = ld(mi + 6), mi7 = ld(mi + 7);
 
             // R_tilde = R + B^T P' B, r_tilde = r + B^T h, S_tilde = B^T P' A (+ rate coupling)
@@ -640,10 +651,16 @@ struct WideSolver {
             const T rt1 = qv7 + (dt * m7[3] + m7[7]);
             const T rdet = rcp(det);
             const T i00 = Rt11 * rdet, i01 = -Rt01 * rdet, i11 = Rt00 * rdet;
-            const T s0j = (hj ? tw * (mc[2] + mc[5]) + mc[6] : cc0j) + hv0j;
-            const T s1j = hj ? dt * mc[3] + mc[7] : cc1j;
-            const T s0i = (hi ? tw * (mi2 + mi5) + mi6 : cc0i) + hv0i;
-            const T s1i = hi ? dt * mi3 + mi7 : cc1i;
+            // (an absent column contributes exact zeros; the coupling entries are zero
+            // on the A_hat columns)
+            T s0j = tw * (mc[2] + mc[5]) + mc[6] + cc0j;
+            const T s1j = dt * mc[3] + mc[7] + cc1j;
+            T s0i = tw * (mi2 + mi5) + mi6 + cc0i;
+            const T s1i = dt * mi3 + mi7 + cc1i;
+            if constexpr (MODEL == 1) {
+                s0j += hv0j;
+                s0i += hv0i;
+            }
             const T K0 = -(i00 * s0j + i01 * s1j);
             const T K1 = -(i01 * s0j + i11 * s1j);
             const T kf0 = -(i00 * rt0 + i01 * rt1);
@@ -658,17 +675,16 @@ struct WideSolver {
                 h1 += c[q + 1] * m7[q + 1];
             }
             const T qh = qh1 + qh2;
-            Pij = qh + (hj ? a0 + a1 : (T)0) + s0i * K0 + s1i * K1;
+            Pij = qh + (a0 + a1) + s0i * K0 + s1i * K1;
             pvi = qvi + (h0 + h1) + s0i * kf0 + s1i * kf1;
             st(sp + t, Pij);
-            if (i == 0) {
-                st(L.KR(k) + j, K0);
-                st(L.KR(k) + 8 + j, K1);
+            // gains K (lanes 0..15: K[0][j], K[1][j]) and k (lanes 16, 17) in one store
+            if (t < 18) {
+                const int a = t < 16 ? L.KR(k) + t : sb + W_::SKF + (t - 16);
+                st(a, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
             }
-            if (t == 0) {
-                st(sb + W_::SKF, kf0);
-                st(sb + W_::SKF + 1, kf1);
-            }
+            wv.sync();  // this stage's reads of M are done
+            st(sm + MS * i + j, gnext);
         }
         // a failed inertia test anywhere (the stages after it computed values the retry overwrites)
         if (wv.uni(bad)) {
