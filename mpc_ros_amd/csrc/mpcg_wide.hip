@@ -97,7 +97,7 @@ hipError_t launch_wide_order(int64_t B, const double* coeffs, void* buf, size_t 
     return e;
 }
 
-size_t wide_lds_bytes(const IpmParams& P) { return (size_t)WideLayout{P.N, P.filter_cap}.total() * sizeof(double); }
+size_t wide_lds_bytes(const IpmParams& P) { return (size_t)WideLayout(P.N, P.filter_cap, P.model).total() * sizeof(double); }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,

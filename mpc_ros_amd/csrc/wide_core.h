@@ -38,9 +38,16 @@
 namespace mpcg {
 
 // LDS layout of one problem (doubles).
+//
+// Stage-major arrays are read and written by stage-parallel lanes (lane k = stage k)
+// with 16-byte accesses.  Their strides are 2 mod 4 doubles (10 for the 8-entry
+// records, 6 for the 6-entry multipliers, 18 for the 16 gains, 42 / 46 for the stage
+// table) so that the 16 lanes of a ds_read_b128 group and the 8 lanes of a
+// ds_write_b128 group hit distinct LDS banks; at a 64-byte stride they conflict 4-way.
 struct WideLayout {
-    int N, cap;
-    static constexpr int SS = 46;  // stage table stride
+    int N, cap, SS;  // SS: stage table stride (42; 46 with the bicycle's turn terms)
+    MPCG_HD WideLayout(int N_, int cap_, int model) : N(N_), cap(cap_), SS(model == 1 ? 46 : 42) {}
+    static constexpr int WS = 10, YS = 6, KS = 18;
     // stage table entries
     static constexpr int SA = 0;    // a[7]: non-trivial entries of A_k (Lin::jac)
     static constexpr int SDT = 7;   // dt
@@ -51,26 +58,26 @@ struct WideLayout {
     static constexpr int SCV = 32;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
     static constexpr int SCC = 37;  // rate coupling C0 C1
     static constexpr int SZERO = 39, SONE = 40, SMONE = 41;  // constants 0, 1, -1
-    // model terms of the heading rows (th, eth): d(turn)/d(w) (B_hat column w: dt for the
-    // differential drive, v/lf dt for the bicycle), d(turn)/d(v) (A_hat column v: 0, w/lf dt),
-    // and the (v, w) curvature of the Lagrangian (0, -(y_th + y_eth)/lf dt)
+    // bicycle only: model terms of the heading rows (th, eth): d(turn)/d(w) (B_hat
+    // column w: v/lf dt; dt for the differential drive), d(turn)/d(v) (A_hat column v:
+    // w/lf dt; 0), and the (v, w) curvature of the Lagrangian (-(y_th + y_eth)/lf dt; 0)
     static constexpr int STW = 42, STV = 43, SHVD = 44;
-    MPCG_HD int W(int k) const { return 8 * k; }
-    MPCG_HD int ZL(int k) const { return 8 * N + 8 * k; }
-    MPCG_HD int ZU(int k) const { return 16 * N + 8 * k; }
-    MPCG_HD int DW(int k) const { return 24 * N + 8 * k; }
-    MPCG_HD int Y(int k) const { return 32 * N + 8 * k; }
-    MPCG_HD int YP(int k) const { return 40 * N + 8 * k; }
-    MPCG_HD int KR(int k) const { return 48 * N + 16 * k; }  // K[0][0..7] K[1][0..7]
-    MPCG_HD int ST(int k) const { return 64 * N + SS * k; }
+    MPCG_HD int W(int k) const { return WS * k; }
+    MPCG_HD int ZL(int k) const { return WS * (N + k); }
+    MPCG_HD int ZU(int k) const { return WS * (2 * N + k); }
+    MPCG_HD int DW(int k) const { return WS * (3 * N + k); }
+    MPCG_HD int Y(int k) const { return 4 * WS * N + YS * k; }
+    MPCG_HD int YP(int k) const { return (4 * WS + YS) * N + YS * k; }
+    MPCG_HD int KR(int k) const { return (4 * WS + 2 * YS) * N + KS * k; }  // K[0][0..7] K[1][0..7]
+    MPCG_HD int ST(int k) const { return (4 * WS + 2 * YS + KS) * N + SS * k; }
     // scratch of the Riccati sweep: G^T of the stage, then M^T (M[r][c] at MS c + r) in
     // the same 8 columns, MS = 10 doubles apart (16-byte column reads of different
     // columns fall in different LDS banks); then P row-major
     static constexpr int MS = 10;
-    MPCG_HD int SCR() const { return (64 + SS) * N; }
-    MPCG_HD int PSC() const { return (64 + SS) * N + 8 * MS; }
-    MPCG_HD int RSC() const { return (64 + SS) * N + 8 * MS + 64; }  // row scales: ra[6] rb[6] 1.0 (+pad)
-    MPCG_HD int ZB() const { return RSC() + 16; }                    // 8 zeros (an absent column)
+    MPCG_HD int SCR() const { return (4 * WS + 2 * YS + KS + SS) * N; }
+    MPCG_HD int PSC() const { return SCR() + 8 * MS; }
+    MPCG_HD int RSC() const { return SCR() + 8 * MS + 64; }  // row scales: ra[6] rb[6] 1.0 (+pad)
+    MPCG_HD int ZB() const { return RSC() + 16; }            // 8 zeros (an absent column)
     MPCG_HD int FI() const { return RSC() + 24; }
     MPCG_HD int total() const { return FI() + 2 * cap; }
 };
@@ -98,7 +105,7 @@ struct WideSolver {
     T lf;  // model 1: wheelbase
 
     MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_)
-        : P(P_), pr(pr_), wv(wv_), L{P_.N, P_.filter_cap}, N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf) {}
+        : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf) {}
 
     // ------------------------------------------------------ the model
     // F(s, u): FG_eval's dynamics (Lin::next); for the bicycle the heading rows turn by
@@ -283,8 +290,10 @@ struct WideSolver {
                 st(L.W(k) + j, push((j < 6 && k == 0) ? pr.init[j] : (T)0, vlo(j), vhi(j)));
                 st(L.ZL(k) + j, 1);
                 st(L.ZU(k) + j, 1);
-                st(L.Y(k) + j, 0);
-                st(L.YP(k) + j, 0);
+                if (j < 6) {
+                    st(L.Y(k) + j, 0);
+                    st(L.YP(k) + j, 0);
+                }
                 st(L.DW(k) + j, 0);
             }
         }
@@ -316,15 +325,15 @@ struct WideSolver {
                 const T hi = j < 6 ? bh[0] : (j == 6 ? bh[1] : bh[2]);
                 if (!(k == N - 1 && j >= 6)) {
                     T wn, zln, zun;
-                    accept_one(ld(L.W(0) + e), ld(L.DW(0) + e), ld(L.ZL(0) + e), ld(L.ZU(0) + e), lo, hi,
+                    accept_one(ld(L.W(k) + j), ld(L.DW(k) + j), ld(L.ZL(k) + j), ld(L.ZU(k) + j), lo, hi,
                                alpha, amax_z, &wn, &zln, &zun);
-                    st(L.W(0) + e, wn);
-                    st(L.ZL(0) + e, zln);
-                    st(L.ZU(0) + e, zun);
+                    st(L.W(k) + j, wn);
+                    st(L.ZL(k) + j, zln);
+                    st(L.ZU(k) + j, zun);
                 }
                 if (j < 6) {
-                    const T y = ld(L.Y(0) + e), yp = ld(L.YP(0) + e);
-                    st(L.Y(0) + e, y + alpha * (yp - y));
+                    const T y = ld(L.Y(k) + j), yp = ld(L.YP(k) + j);
+                    st(L.Y(k) + j, y + alpha * (yp - y));
                 }
             }
         }
@@ -379,9 +388,11 @@ struct WideSolver {
             }
 #pragma unroll
             for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cvk[j]);
-            st(sb + WideLayout::STW, twk);
-            st(sb + WideLayout::STV, tvk);
-            st(sb + WideLayout::SHVD, hvdk);
+            if constexpr (MODEL == 1) {
+                st(sb + WideLayout::STW, twk);
+                st(sb + WideLayout::STV, tvk);
+                st(sb + WideLayout::SHVD, hvdk);
+            }
             if (k >= 1) {
                 um[0] = ld(L.W(k - 1) + 6);
                 um[1] = ld(L.W(k - 1) + 7);
@@ -473,9 +484,11 @@ struct WideSolver {
             }
 #pragma unroll
             for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
-            st(sb + WideLayout::STW, tw);
-            st(sb + WideLayout::STV, tv);
-            st(sb + WideLayout::SHVD, 0);
+            if constexpr (MODEL == 1) {
+                st(sb + WideLayout::STW, tw);
+                st(sb + WideLayout::STV, tv);
+                st(sb + WideLayout::SHVD, 0);
+            }
 #pragma unroll
             for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, 0);
 #pragma unroll
@@ -538,14 +551,16 @@ struct WideSolver {
     MPCG_HD static int goff(int s, int m) {
         typedef WideLayout W_;
         const int Z = W_::SZERO, O = W_::SONE, A = W_::SA, D = W_::SD;
+        // (differential drive: d turn / d w = dt, d turn / d v = 0)
+        const int TW = MODEL == 1 ? W_::STW : W_::SDT, TV = MODEL == 1 ? W_::STV : W_::SZERO;
         int o = Z;
         o = (s == 0) ? (m == 0 ? O : (m == 4 ? A + 4 : Z)) : o;
         o = (s == 1) ? (m == 1 ? O : (m == 4 ? W_::SMONE : Z)) : o;
         o = (s == 2) ? (m == 0 ? A + 0 : (m == 1 ? A + 2 : (m == 2 ? O : Z))) : o;
-        o = (s == 3) ? (m == 0 ? A + 1 : (m == 1 ? A + 3 : (m == 3 ? O : (m == 4 ? A + 5 : ((m == 2 || m == 5) ? W_::STV : Z))))) : o;
+        o = (s == 3) ? (m == 0 ? A + 1 : (m == 1 ? A + 3 : (m == 3 ? O : (m == 4 ? A + 5 : ((m == 2 || m == 5) ? TV : Z))))) : o;
         o = (s == 4) ? (m == 4 ? A + 6 : (m == 5 ? O : Z)) : o;
         // B_hat: w -> tw e2 + tw e5 + e6 (tw = d turn / d w) ; a -> dt e3 + e7
-        o = (s == 5) ? ((m == 2 || m == 5) ? W_::STW : (m == 6 ? O : Z)) : o;
+        o = (s == 5) ? ((m == 2 || m == 5) ? TW : (m == 6 ? O : Z)) : o;
         o = (s == 6) ? (m == 3 ? W_::SDT : (m == 7 ? O : Z)) : o;
         o = (s == 7) ? (m < 6 ? D + m : Z) : o;
         return o;
@@ -724,7 +739,10 @@ struct WideSolver {
             ldv<2>(L.ST(t) + WideLayout::SKF, kf);
             ldv<8>(L.ST(t) + WideLayout::SA, a);
             ldv<6>(L.ST(t) + WideLayout::SD, d);
-            ld2(L.ST(t) + WideLayout::STW, twl, tvl);
+            if constexpr (MODEL == 1)
+                ld2(L.ST(t) + WideLayout::STW, twl, tvl);
+            else
+                twl = dt;
         } else {  // last stage (and idle lanes): no control, du = 0
 #pragma unroll
             for (int q = 0; q < 16; ++q) K[q] = 0;
@@ -802,8 +820,10 @@ struct WideSolver {
                 ldv<8>(sb + WideLayout::SQV, qv);
                 ldv<6>(sb + WideLayout::SCV, cv);  // cv[0..4] = Q00 Q22 Q32 Q55 Q53
                 ldv<8>(sb + WideLayout::SA, ak);
-                tva = ld(sb + WideLayout::STV);
-                hvd = ld(sb + WideLayout::SHVD);
+                if constexpr (MODEL == 1) {
+                    tva = ld(sb + WideLayout::STV);
+                    hvd = ld(sb + WideLayout::SHVD);
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) { qd[q] = 0; qv[q] = 0; ak[q] = 0; }

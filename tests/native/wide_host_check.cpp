@@ -90,7 +90,7 @@ int main() {
     if (std::scanf("%d %lf", &P.model, &P.lf) != 2) return 1;
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
-    const mpcg::WideLayout L{P.N, P.filter_cap};
+    const mpcg::WideLayout L(P.N, P.filter_cap, P.model);
     for (long b = 0; b < B; ++b) {
         mpcg::IpmProblem<double> pr;
         for (double& v : pr.init) std::scanf("%lf", &v);

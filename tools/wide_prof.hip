@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dst, st.data(), B * 6 * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dcf, cf.data(), B * 4 * 8, hipMemcpyHostToDevice));
     CK(hipMemset(dacc, 0, B * W * 8));
-    const size_t lds = (size_t)mpcg::WideLayout{P.N, P.filter_cap}.total() * 8;
+    const size_t lds = (size_t)mpcg::WideLayout(P.N, P.filter_cap, P.model).total() * 8;
     CK(hipFuncSetAttribute((const void*)mpcg::k_prof, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
