@@ -11,7 +11,8 @@
 //                   a commutative op leaves every lane with identical bits;
 //   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
 //   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
-//   S()             the LDS base (address 0); ld2(i, a, b): 16-byte LDS load of two doubles (i even).
+//   S()             the LDS base (address 0); ld2(i, a, b) / st2(i, a, b): 16-byte LDS load /
+//                   store of two doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
 #define MPCG_WAVE_DEV_H
 
@@ -47,6 +48,9 @@ struct DevWaveBase {
         const double2 v = *(const ldsT2*)(S() + i);
         a = v.x;
         b = v.y;
+    }
+    __device__ __forceinline__ void st2(int i, double a, double b) const {
+        *(ldsT2*)(S() + i) = double2{a, b};
     }
     template <int pat>
     __device__ __forceinline__ static double swz(double v) {

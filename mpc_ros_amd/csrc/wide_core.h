@@ -784,8 +784,10 @@ struct WideSolver {
             }
             T y[8];
             A_mul(a, x, y);
-            y[2] += tvl * x[3];
-            y[5] += tvl * x[3];
+            if constexpr (MODEL == 1) {
+                y[2] += tvl * x[3];
+                y[5] += tvl * x[3];
+            }
             y[2] += twl * du0;
             y[3] += dt * du1;
             y[5] += twl * du0;
@@ -837,14 +839,14 @@ struct WideSolver {
             base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
             base[4] = qd[4] * x[4] + qv[4];
             base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
-            base[3] += hvd * duk[0];  // (v, w) curvature times the stage's w step (bicycle)
+            if constexpr (MODEL == 1) base[3] += hvd * duk[0];  // (v, w) curvature times the w step
         }
 #pragma unroll
         for (int q = 0; q < 6; ++q) { lam[q] = 0; lk[q] = 0; }
         for (int s = N - 1; s >= 0; --s) {
             T o[6];
             AT_mul(ak, lam, o);
-            o[3] += tva * (lam[2] + lam[5]);
+            if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) o[q] += base[q];
             if (t == s) {

@@ -56,6 +56,10 @@ struct HostWave {
         a = lds[i];
         b = lds[i + 1];
     }
+    void st2(int i, double a, double b) const {
+        lds[i] = a;
+        lds[i + 1] = b;
+    }
     double from(double v, int src) const {
         sh->xd[t] = v;
         sync();
