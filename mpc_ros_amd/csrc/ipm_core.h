@@ -185,10 +185,12 @@ MPCG_HD void sc_t(T a, T* s, T* c) {
         sincos_large(a, s, c);  // out of line: never reached by a bounded trajectory
 }
 
+// max / min with C fmax / fmin (IEEE maxNum) semantics, as the oracle: one v_max_f64 /
+// v_min_f64 on the device (a compare and two selects otherwise)
 template <typename T>
-MPCG_HD T tmax(T a, T b) { return a > b ? a : b; }
+MPCG_HD T tmax(T a, T b) { return fmax(a, b); }
 template <typename T>
-MPCG_HD T tmin(T a, T b) { return a < b ? a : b; }
+MPCG_HD T tmin(T a, T b) { return fmin(a, b); }
 
 // Reciprocal: on the device v_rcp_f64 refined by two Newton steps (5 instructions,
 // within an ulp of 1/x) instead of the ~10-instruction correctly rounded division;

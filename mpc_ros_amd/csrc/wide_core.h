@@ -245,11 +245,13 @@ struct WideSolver {
     }
     MPCG_HD void bounds_only() {
         const T rl = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.bound));
-        sl0 = (T)-P.bound; su0 = (T)P.bound; sl = sl0 - rl; su = su0 + rl;
+        // (uniform values made scalar: the register allocator keeps them in SGPRs rather
+        // than spilling vector copies to scratch)
+        sl0 = wv.uni_d((T)-P.bound); su0 = wv.uni_d((T)P.bound); sl = wv.uni_d(sl0 - rl); su = wv.uni_d(su0 + rl);
         const T rw = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_w));
-        wl0 = (T)-P.max_w; wu0 = (T)P.max_w; wl = wl0 - rw; wu = wu0 + rw;
+        wl0 = wv.uni_d((T)-P.max_w); wu0 = wv.uni_d((T)P.max_w); wl = wv.uni_d(wl0 - rw); wu = wv.uni_d(wu0 + rw);
         const T rA = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_a));
-        al0 = (T)-P.max_a; au0 = (T)P.max_a; al = al0 - rA; au = au0 + rA;
+        al0 = wv.uni_d((T)-P.max_a); au0 = wv.uni_d((T)P.max_a); al = wv.uni_d(al0 - rA); au = wv.uni_d(au0 + rA);
     }
     MPCG_HD void setup() {
         bounds_only();
@@ -973,8 +975,8 @@ struct WideSolver {
     MPCG_HD void init() {
         setup();
         init_point();
-        mu = (T)P.mu_init;
-        tau = tmax((T)0.99, (T)1 - (T)P.mu_init);
+        mu = wv.uni_d((T)P.mu_init);
+        tau = wv.uni_d(tmax((T)0.99, (T)1 - (T)P.mu_init));
         status = 0;
         // least-squares multipliers (constr_mult_init_max 1000)
         const bool ok = riccati(1, (T)0);
@@ -996,8 +998,8 @@ struct WideSolver {
             for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
         }
         stats(false, (T)0, (T)0);
-        theta_max = (T)1e4 * tmax((T)1, theta);
-        theta_min = (T)1e-4 * tmax((T)1, theta);
+        theta_max = wv.uni_d((T)1e4 * tmax((T)1, theta));
+        theta_min = wv.uni_d((T)1e-4 * tmax((T)1, theta));
         dw_last = 0;
         acc_alpha = 0;
         acc_z = 0;
@@ -1014,7 +1016,7 @@ struct WideSolver {
         const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
         const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
         const T dual_uns = dual_inf / sf;
-        kkt = tmax(dual_uns, tmax(prim_uns, compl0));
+        kkt = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl0)));
         int s = 0;
         // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
         // drop a NaN; the sums do not)
@@ -1049,13 +1051,13 @@ struct WideSolver {
         for (;;) {
             if (riccati(0, delta_w)) {
                 ok = true;
-                if (delta_w > 0) dw_last = delta_w;
+                if (delta_w > 0) dw_last = wv.uni_d(delta_w);
                 break;
             }
             if (attempt == 0)
-                delta_w = (dw_last == 0) ? (T)1e-4 : tmax((T)1e-20, dw_last / (T)3);
+                delta_w = wv.uni_d((dw_last == 0) ? (T)1e-4 : tmax((T)1e-20, dw_last / (T)3));
             else
-                delta_w = (dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
+                delta_w = wv.uni_d((dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w);
             ++attempt;
             if (wv.uni(delta_w > (T)1e40)) break;
         }
@@ -1134,8 +1136,8 @@ struct WideSolver {
                 st(fi + 2 * slot + 1, phik - gamma_phi * thetak);
             }
         }
-        acc_alpha = alpha;
-        acc_z = F.amax_z;
+        acc_alpha = wv.uni_d(alpha);
+        acc_z = wv.uni_d(F.amax_z);
         wv.mark(7);
         return 0;
     }
