@@ -84,6 +84,39 @@ def cpu_baseline(P, st, cf, budget_s):
                 iters_mean=float(np.mean(r["iters"])))
 
 
+def latency_b1(P, st, cf, solver, dev, reps=50):
+    """One robot per call (the reference's use: one MPC::Solve per control tick):
+    device-resident launch-to-completion, the host-buffer path (copies included),
+    and the oracle on one host thread; medians over repetitions of problem 0."""
+    import torch
+
+    from oracle import pyoracle as O
+
+    s1, c1 = st[:1], cf[:1]
+    ts, tc = torch.from_numpy(s1).to(dev), torch.from_numpy(c1).to(dev)
+    u = torch.empty((1, 2), dtype=torch.float64, device=dev)
+    dev_ms, host_ms, cpu_ms = [], [], []
+    for r in range(reps + 5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        solver.solve_device(ts, tc, u)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        solver.solve(s1, c1)
+        t2 = time.perf_counter()
+        if r >= 5:
+            dev_ms.append((t1 - t0) * 1e3)
+            host_ms.append((t2 - t1) * 1e3)
+    opts = O.ipm_opts(tol=1e-8)
+    for r in range(min(reps, 20)):
+        t0 = time.perf_counter()
+        O.mpc_solve_batch(P, s1, c1, opts=opts, nthreads=1)
+        cpu_ms.append((time.perf_counter() - t0) * 1e3)
+    return {"gpu_device_ms": float(np.median(dev_ms)), "gpu_host_buffers_ms": float(np.median(host_ms)),
+            "cpu_oracle_ms": float(np.median(cpu_ms)),
+            "sample": f"problem 0 of the batch, B = 1, median of {reps} (GPU) / {min(reps, 20)} (CPU, 1 thread)"}
+
+
 def pmc_profile(name):
     path = os.path.join(ROOT, "profiles", f"{name}.json")
     if not os.path.exists(path):
@@ -220,6 +253,7 @@ def main():
         }
         if world == 1 and a.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(P, st, cf, a.cpu_seconds)
+            line["latency_b1"] = latency_b1(P, st, cf, solver, dev)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
