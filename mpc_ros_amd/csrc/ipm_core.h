@@ -1154,9 +1154,11 @@ struct IpmSolver {
                     if (thetat >= fth && phit >= fph) { infilt = true; break; }
                 }
                 if (!infilt) {
-                    const bool sw = (gd < 0) && (alpha * (T)pow((double)-gd, (double)s_phi) >
-                                                 delta_sw * (T)pow((double)thetak, (double)s_theta));
-                    if (thetak <= theta_min && sw) {
+                    // (the powers are evaluated only where the switching condition is read)
+                    const bool sw = (thetak <= theta_min) && (gd < 0) &&
+                                    (alpha * (T)pow((double)-gd, (double)s_phi) >
+                                     delta_sw * (T)pow((double)thetak, (double)s_theta));
+                    if (sw) {
                         if (phit <= phik + eta_phi * alpha * gd) { accepted = true; ftype = true; break; }
                     } else if (thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak) {
                         accepted = true;

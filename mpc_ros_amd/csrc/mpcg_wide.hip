@@ -28,7 +28,8 @@ struct WideArgs {
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
 // budget of 256 per lane lets all of them be resident
-template <int MODEL>
+// SPLIT (N <= 32): the recursions and the step statistics use both half-waves (wide_core.h)
+template <int MODEL, bool SPLIT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
@@ -40,7 +41,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int j = 0; j < 4; ++j) pr.c[j] = a.coeffs[p * 4 + j];
     DevWave wv;
     wv.t = t;
-    WideSolver<DevWave, MODEL> S(a.P, pr, wv);
+    WideSolver<DevWave, MODEL, SPLIT> S(a.P, pr, wv);
     S.solve();
     const double o = S.objective_out();
     const int N = a.P.N;
@@ -104,7 +105,9 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
                              hipStream_t stream) {
     if (B <= 0) return hipSuccess;
     const size_t lds = wide_lds_bytes(P);
-    const void* fn = P.model == 1 ? (const void*)k_solve_wide<1> : (const void*)k_solve_wide<0>;
+    const bool split = P.N <= 32;
+    const void* fn = P.model == 1 ? (split ? (const void*)k_solve_wide<1, true> : (const void*)k_solve_wide<1, false>)
+                                  : (split ? (const void*)k_solve_wide<0, true> : (const void*)k_solve_wide<0, false>);
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -113,10 +116,14 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters};
-    if (P.model == 1)
-        hipLaunchKernelGGL(k_solve_wide<1>, dim3((unsigned)B), dim3(64), lds, stream, a);
+    if (P.model == 1 && split)
+        hipLaunchKernelGGL((k_solve_wide<1, true>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    else if (P.model == 1)
+        hipLaunchKernelGGL((k_solve_wide<1, false>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    else if (split)
+        hipLaunchKernelGGL((k_solve_wide<0, true>), dim3((unsigned)B), dim3(64), lds, stream, a);
     else
-        hipLaunchKernelGGL(k_solve_wide<0>, dim3((unsigned)B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((k_solve_wide<0, false>), dim3((unsigned)B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 

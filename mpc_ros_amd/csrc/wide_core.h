@@ -84,7 +84,10 @@ struct WideLayout {
 
 // MODEL: 0 differential drive (FG_eval), 1 kinematic bicycle -- a template parameter
 // so that the differential-drive kernel carries none of the bicycle's terms.
-template <class WV, int MODEL = 0>
+// SPLIT (N <= 32): the step and multiplier recursions run in both half-waves (lane t and
+// t + 32 hold stage t & 31), and the step statistics take the stage's variables 0..3 in
+// the lower and 4..7 in the upper half-wave: half the per-variable work per lane.
+template <class WV, int MODEL = 0, bool SPLIT = false>
 struct WideSolver {
     typedef double T;
     const IpmParams P;
@@ -145,22 +148,30 @@ struct WideSolver {
     template <int s, int n>
     MPCG_HD void rstep(T* v, const int* op) {
         T o[n];
+        if constexpr (s == 5) {
+            // across the half-waves: {v, o} = {own, partner} in some order (a commutative op
+            // leaves both lanes of the pair with the same bits)
 #pragma unroll
-        for (int q = 0; q < n; ++q) o[q] = wv.template rpart<s>(v[q]);
+            for (int q = 0; q < n; ++q) wv.xor32_pair(v[q], v[q], o[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < n; ++q) o[q] = wv.template rpart<s>(v[q]);
+        }
 #pragma unroll
         for (int q = 0; q < n; ++q)
             v[q] = op[q] == RSUM ? v[q] + o[q] : (op[q] == RMAX ? tmax(v[q], o[q]) : tmin(v[q], o[q]));
     }
-    // Contributions come from lanes < N only: for N <= 32 five steps complete the
-    // reduction in lanes 0..31 and lane 0's value is made wave-uniform (scalar).
-    template <int n>
+    // Contributions come from lanes < N only (FULL: from both half-waves): for N <= 32
+    // five steps complete the reduction in lanes 0..31 and lane 0's value is made
+    // wave-uniform (scalar).
+    template <int n, bool FULL = false>
     MPCG_HD void reduce(T* v, const int* op) {
         rstep<0, n>(v, op);
         rstep<1, n>(v, op);
         rstep<2, n>(v, op);
         rstep<3, n>(v, op);
         rstep<4, n>(v, op);
-        if (N > 32) rstep<5, n>(v, op);
+        if (FULL || N > 32) rstep<5, n>(v, op);
 #pragma unroll
         for (int q = 0; q < n; ++q) v[q] = wv.uni_d(v[q]);
     }
@@ -729,20 +740,80 @@ struct WideSolver {
         F.rel = tmax(F.rel, (T)fabs(dwv) * rcp((T)1 + (T)fabs(w)));
     }
 
+    // Lane masks of the systolic recursions (bit t: lane t keeps its vector this step):
+    // stages k <= s (step recursion) / k >= s (multiplier recursion), in both half-waves
+    // when SPLIT.
+    MPCG_HD unsigned long long keep_up(int s) const {
+        if constexpr (SPLIT) {
+            const unsigned long long m = s >= 31 ? 0xFFFFFFFFull : ((2ull << s) - 1);
+            return m | (m << 32);
+        } else {
+            return s >= 63 ? ~0ull : ((2ull << s) - 1);
+        }
+    }
+    MPCG_HD unsigned long long keep_dn(int s) const {
+        if constexpr (SPLIT) {
+            const unsigned long long m = (0xFFFFFFFFull << s) & 0xFFFFFFFFull;
+            return m | (m << 32);
+        } else {
+            return ~0ull << s;
+        }
+    }
+    // Step statistics of stage k (SPLIT): the lower half-wave takes variables 0..3 (x, y,
+    // theta, v), the upper 4..7 (cte, etheta, w, a); same per-variable formulas as the
+    // unsplit sweep below (gradient of the barrier function, dir_var).
+    MPCG_HD void step_stats_split(int k, const T* xk, const T* duk, Fwd& F) const {
+        const bool hi = t >= 32, last = k == N - 1;
+        const int j0 = hi ? 4 : 0;
+        T w[4], zl[4], zu[4];
+        ldv<4>(L.W(k) + j0, w);
+        ldv<4>(L.ZL(k) + j0, zl);
+        ldv<4>(L.ZU(k) + j0, zu);
+        // gradient of the objective (scaled): g[3] (lower) / g[4], g[5], gu (upper)
+        T gu[2] = {0, 0};
+        if (!last) {
+            T um[2] = {0, 0}, up[2];
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            up[0] = ld(L.W(k + 1) + 6);
+            up[1] = ld(L.W(k + 1) + 7);
+            const T u[2] = {w[2], w[3]};  // (upper half: variables 6, 7)
+            grad_ctrl(k, um, u, up, gu);
+        }
+        const T g4 = (T)(2.0 * P.w_cte) * (w[0] - (T)P.ref_cte), g5 = (T)(2.0 * P.w_eth) * (w[1] - (T)P.ref_eth);
+        const T g3 = (T)(2.0 * P.w_v) * (w[3] - (T)P.ref_v);
+        const T gq[4] = {hi ? sf * g4 : sf * (T)0, hi ? sf * g5 : sf * (T)0, hi ? sf * gu[0] : sf * (T)0,
+                         hi ? sf * gu[1] : sf * g3};
+        const T dq[4] = {hi ? xk[4] : xk[0], hi ? xk[5] : xk[1], hi ? duk[0] : xk[2], hi ? duk[1] : xk[3]};
+        const T lo2 = hi ? wl : sl, hi2 = hi ? wu : su, lo3 = hi ? al : sl, hi3 = hi ? au : su;
+        const int nv = (last && hi) ? 2 : 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q < nv) {
+                const T lo = q < 2 ? sl : (q == 2 ? lo2 : lo3), up_ = q < 2 ? su : (q == 2 ? hi2 : hi3);
+                const T gphi = gq[q] - mu * rcp(w[q] - lo) + mu * rcp(up_ - w[q]);
+                dir_var(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], F);
+            }
+        }
+    }
+
     MPCG_HD Fwd forward(int mode) {
         wv.sync();
         // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
         // systolically: lane k holds stage k's records, every step every lane applies its
         // own stage map to the vector it holds and passes the result one lane up, so lane
         // k sees its correct input at step k (and keeps it).
+        const int ks = SPLIT ? (t & 31) : t;  // the lane's stage
         T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
-        if (t < N - 1) {
-            ldv<16>(L.KR(t), K);
-            ldv<2>(L.ST(t) + WideLayout::SKF, kf);
-            ldv<8>(L.ST(t) + WideLayout::SA, a);
-            ldv<6>(L.ST(t) + WideLayout::SD, d);
+        if (ks < N - 1) {
+            ldv<16>(L.KR(ks), K);
+            ldv<2>(L.ST(ks) + WideLayout::SKF, kf);
+            ldv<8>(L.ST(ks) + WideLayout::SA, a);
+            ldv<6>(L.ST(ks) + WideLayout::SD, d);
             if constexpr (MODEL == 1)
-                ld2(L.ST(t) + WideLayout::STW, twl, tvl);
+                ld2(L.ST(ks) + WideLayout::STW, twl, tvl);
             else
                 twl = dt;
         } else {  // last stage (and idle lanes): no control, du = 0
@@ -755,19 +826,19 @@ struct WideSolver {
 #pragma unroll
             for (int q = 0; q < 6; ++q) d[q] = 0;
         }
-        T x[8], xk[8], duk[2];
+        T x[8];
         {
             T w0[6];
             ldn<6>(L.W(0), w0);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && t == 0) ? -(w0[j] - pr.init[j]) : (T)0;
+            for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && ks == 0) ? -(w0[j] - pr.init[j]) : (T)0;
             x[6] = 0;
             x[7] = 0;
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) xk[q] = 0;
-        duk[0] = 0;
-        duk[1] = 0;
+        // Lane k's input is correct at step k; from then on the lane keeps it (the shift
+        // writes only lanes above the current step), so after the last step every lane
+        // holds its own stage's step and, recomputed from it, its control step.
+        T du0 = 0, du1 = 0;
         for (int s = 0; s < N; ++s) {
             T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
 #pragma unroll
@@ -777,13 +848,8 @@ struct WideSolver {
                 u1a += K[8 + m] * x[m];
                 u1b += K[9 + m] * x[m + 1];
             }
-            const T du0 = u0a + u0b, du1 = u1a + u1b;
-            if (t == s) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) xk[q] = x[q];
-                duk[0] = du0;
-                duk[1] = du1;
-            }
+            du0 = u0a + u0b;
+            du1 = u1a + u1b;
             T y[8];
             A_mul(a, x, y);
             if constexpr (MODEL == 1) {
@@ -797,9 +863,10 @@ struct WideSolver {
             for (int j = 0; j < 6; ++j) y[j] += d[j];
             y[6] = du0;
             y[7] = du1;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] = wv.up1(y[q]);
+            wv.up8_keep(x, y, keep_up(s));
         }
+        const T* xk = x;
+        const T duk[2] = {du0, du1};
         if (t < N) {
 #pragma unroll
             for (int j = 0; j < 6; j += 2) {
@@ -815,11 +882,11 @@ struct WideSolver {
         // (rows 0..5 of the Riccati costate P_k ds_k + p_k), a backward systolic pass:
         // lane k holds stage k's Hessian diagonal and curvature, gradient and A_k.
         wv.mark(3);
-        T lam[6], lk[6], base[6], ak[8], tva = 0;
+        T lam[6], base[6], ak[8], tva = 0;
         {
             T qd[8], qv[8], cv[6], hvd = 0;
-            if (t < N) {
-                const int sb = L.ST(t);
+            if (ks < N) {
+                const int sb = L.ST(ks);
                 ldv<8>(sb + WideLayout::SQD, qd);
                 ldv<8>(sb + WideLayout::SQV, qv);
                 ldv<6>(sb + WideLayout::SCV, cv);  // cv[0..4] = Q00 Q22 Q32 Q55 Q53
@@ -844,27 +911,26 @@ struct WideSolver {
             if constexpr (MODEL == 1) base[3] += hvd * duk[0];  // (v, w) curvature times the w step
         }
 #pragma unroll
-        for (int q = 0; q < 6; ++q) { lam[q] = 0; lk[q] = 0; }
+        for (int q = 0; q < 6; ++q) lam[q] = 0;
+        // (as the step recursion: lane k keeps its multiplier input from step k on, so the
+        // last step's output in lane k is stage k's)
+        T o[6];
         for (int s = N - 1; s >= 0; --s) {
-            T o[6];
             AT_mul(ak, lam, o);
             if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) o[q] += base[q];
-            if (t == s) {
-#pragma unroll
-                for (int q = 0; q < 6; ++q) lk[q] = o[q];
-            }
-#pragma unroll
-            for (int q = 0; q < 6; ++q) lam[q] = wv.dn1(o[q]);
+            wv.dn6_keep(lam, o, keep_dn(s));
         }
         if (t < N) {
 #pragma unroll
-            for (int q = 0; q < 6; ++q) st(L.YP(t) + q, -lk[q]);
+            for (int q = 0; q < 6; ++q) st(L.YP(t) + q, -o[q]);
         }
         wv.mark(4);
         Fwd F{(T)1, (T)1, (T)0, (T)0};
-        if (t < N) {
+        if constexpr (SPLIT) {
+            if (mode == 0 && ks < N) step_stats_split(ks, xk, duk, F);
+        } else if (t < N) {
             const int k = t;
             const bool last = k == N - 1;
             if (mode == 0) {
@@ -902,7 +968,7 @@ struct WideSolver {
         if (mode == 0) {
             T v[4] = {F.amax_p, F.amax_z, F.gd, F.rel};
             const int op[4] = {RMIN, RMIN, RSUM, RMAX};
-            reduce<4>(v, op);
+            reduce<4, SPLIT>(v, op);
             F.amax_p = v[0];
             F.amax_z = v[1];
             F.gd = v[2];
@@ -1071,9 +1137,11 @@ struct WideSolver {
         const T thetak = theta;
         const T gd = F.gd;
         const int cap = P.filter_cap;
-        // the switching-condition powers are loop invariants of the trial loop
+        // the switching-condition powers are loop invariants of the trial loop, and are
+        // read only when theta_k <= theta_min (the switching condition and alpha_min's
+        // third term); an inlined pow is ~250 instructions, so they are computed only then
         T pgd = 0, pth = 0;
-        if (wv.uni(gd < 0)) {
+        if (wv.uni(gd < 0 && thetak <= theta_min)) {
             pgd = wv.uni_d((T)pow((double)-gd, (double)s_phi));
             pth = wv.uni_d((T)pow((double)thetak, (double)s_theta));
         }

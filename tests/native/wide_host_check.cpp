@@ -68,6 +68,24 @@ struct HostWave {
         return r;
     }
     double dn1(double v) const { return from(v, t < 63 ? t + 1 : t); }
+    void up8_keep(double* x, const double* y, unsigned long long keep) const {
+        for (int q = 0; q < 8; ++q) {
+            const double r = up1(y[q]);
+            if (!((keep >> t) & 1)) x[q] = r;
+        }
+    }
+    void dn6_keep(double* x, const double* y, unsigned long long keep) const {
+        for (int q = 0; q < 6; ++q) {
+            const double r = dn1(y[q]);
+            if (!((keep >> t) & 1)) x[q] = r;
+        }
+    }
+    // device: v_permlane32_swap gives the lower half (own, partner), the upper (partner, own)
+    void xor32_pair(double v, double& a, double& b) const {
+        const double o = from(v, t ^ 32);
+        a = t < 32 ? v : o;
+        b = t < 32 ? o : v;
+    }
     double uni_d(double v) const { return from(v, 0); }
     template <int q>
     double bcast8(double v) const { return from(v, (t & ~7) | q); }
@@ -121,11 +139,17 @@ int main() {
                             for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
                     }
                 };
-                if (P.model == 1) {
-                    mpcg::WideSolver<HostWave, 1> S(P, pr, wv);
+                if (P.model == 1 && P.N <= 32) {
+                    mpcg::WideSolver<HostWave, 1, true> S(P, pr, wv);
+                    run(S);
+                } else if (P.model == 1) {
+                    mpcg::WideSolver<HostWave, 1, false> S(P, pr, wv);
+                    run(S);
+                } else if (P.N <= 32) {
+                    mpcg::WideSolver<HostWave, 0, true> S(P, pr, wv);
                     run(S);
                 } else {
-                    mpcg::WideSolver<HostWave, 0> S(P, pr, wv);
+                    mpcg::WideSolver<HostWave, 0, false> S(P, pr, wv);
                     run(S);
                 }
             });

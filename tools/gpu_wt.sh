@@ -1,11 +1,14 @@
-# Time every built tools/wt_<variant> on the benchmark inputs; outputs compared to wt_base.
+# Time built tools/wt_<variant> binaries on the benchmark inputs (outputs compared to the
+# first one); each variant is timed twice, interleaved, to expose drift between runs.
+#   WT_VARIANTS="base orig" bash tools/gpu_wt.sh
 set -u
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out/wt
-timeout -k 10 120 ./tools/wt_base tools/inputs_65536.bin gpurun_out/wt/base.bin || exit 1
-for v in ${WT_VARIANTS:-}; do
-  echo "== $v"
-  timeout -k 10 120 ./tools/wt_$v tools/inputs_65536.bin gpurun_out/wt/$v.bin gpurun_out/wt/base.bin || exit 1
+set -- ${WT_VARIANTS:-base}
+ref=$1
+for pass in 1 2; do
+  for v in "$@"; do
+    echo "== $v ($pass)"
+    timeout -k 10 120 ./tools/wt_$v tools/inputs_65536.bin gpurun_out/wt/$v.bin gpurun_out/wt/$ref.bin || exit 1
+  done
 done
-echo "== base again"
-timeout -k 10 120 ./tools/wt_base tools/inputs_65536.bin gpurun_out/wt/base2.bin gpurun_out/wt/base.bin

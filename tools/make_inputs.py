@@ -1,0 +1,21 @@
+"""Write the benchmark batch as tools/inputs_<B>.bin ([int64 B][B x 6 state][B x 4 coeffs]),
+the input format of the diagnostic tools (wide_time.hip, wide_prof.hip).
+
+    python tools/make_inputs.py [B]
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mpc_ros_amd import infinity  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+st, cf = infinity.make_problems(np.arange(B))
+out = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"inputs_{B}.bin")
+with open(out, "wb") as f:
+    f.write(np.int64(B).tobytes())
+    f.write(np.ascontiguousarray(st, dtype=np.float64).tobytes())
+    f.write(np.ascontiguousarray(cf, dtype=np.float64).tobytes())
+print(out)

@@ -50,6 +50,30 @@ __global__ void __launch_bounds__(64) k(double* out, long long* cyc, int n, doub
                 rr = __builtin_fma(rr, e, rr);
                 x = __builtin_fma(rr, b, a);
             }
+        } else if (KIND == 6) {  // 16 independent FMA chains (issue rate of FP64 FMA)
+            double y[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) y[r] = x + r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) y[r] = __builtin_fma(y[r], b, a);
+            double z = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) z += y[r];
+            x = z;
+        } else if (KIND == 7) {  // 16 independent 32-bit integer chains (issue rate of v_add_u32 / v_xor)
+            unsigned u[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) u[r] = __double2loint(x) + r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) u[r] = (u[r] * 3u) ^ (unsigned)q;
+            unsigned z = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) z ^= u[r];
+            x = __hiloint2double(__double2hiint(x), (int)z);
         } else if (KIND == 5) {  // FMA + readfirstlane (uniform)
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
@@ -86,13 +110,15 @@ void run(const char* name, int waves_per_simd, int ops_per_iter) {
 }
 
 int main() {
-    for (int w = 1; w <= 2; ++w) {
+    for (int w = 1; w <= 4; w *= 2) {
         run<0>("fma f64 dependent", w, 8);
         run<1>("fma f64 8 independent chains", w, 64);
         run<2>("fma + dpp wave_shr (per pair)", w, 8);
         run<3>("fma + lds write/read (per pair)", w, 8);
         run<4>("rcp+2 newton+fma (per 6 ops)", w, 2);
         run<5>("fma + readfirstlane x2 (per pair)", w, 8);
+        run<6>("fma f64 16 independent chains", w, 64);
+        run<7>("u32 mul+xor 16 chains (per mul+xor)", w, 64);
     }
     return 0;
 }

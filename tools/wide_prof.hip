@@ -6,6 +6,7 @@
 // defaults, N = 20).  Prints per-phase cycles per solve and per iteration.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I mpc_ros_amd/csrc tools/wide_prof.hip -o wide_prof
+//   (or bash tools/build_wp.sh base v1 ...: the product sources or variants/<name>/)
 //   ./wide_prof inputs.bin [B_limit]
 #include <hip/hip_runtime.h>
 
@@ -14,12 +15,14 @@
 #include <algorithm>
 #include <vector>
 
-#include "../mpc_ros_amd/csrc/wave_dev.h"
-#include "../mpc_ros_amd/csrc/wide_core.h"
+#include "wave_dev.h"
+#include "wide_core.h"
 
 namespace mpcg {
-constexpr int NPH = 9;
-const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest"};
+constexpr int NPH = 14;
+// 9..13: sub-phase stamps of diagnostic variants (variants/stamps)
+const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest",
+                           "st-accept", "st-eval", "st-vars", "ric-M", "ric-KP"};
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
@@ -48,7 +51,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     wv.last = (unsigned long long)clock64();
     const unsigned long long t0 = wv.last;
     const unsigned long long r0 = wall_clock64();
-    WideSolver<ProfWave> S(P, pr, wv);
+    WideSolver<ProfWave, 0, true> S(P, pr, wv);  // (N = 20: SPLIT)
     S.solve();
     if (threadIdx.x == 0) {
         times[2 * p] = r0;
