@@ -14,6 +14,10 @@
 //                   mask m, which keep x (the systolic recursions);
 //   xor32_pair(v, a, b)  {a, b} = {v, v of lane t ^ 32} (v_permlane32_swap);
 //   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
+//   lane()          the lane index, recomputed by a volatile v_mbcnt pair: each solver phase
+//                   derives its per-lane LDS offsets from it, so the compiler cannot hoist
+//                   them out of the iteration loop (they were kept live across every phase
+//                   and 60-70 VGPRs spilled to scratch);
 //   S()             the LDS base (address 0); ld2(i, a, b) / st2(i, a, b): 16-byte LDS load /
 //                   store of two doubles (i even).
 #ifndef MPCG_WAVE_DEV_H
@@ -165,6 +169,13 @@ struct DevWaveBase {
         b = __hiloint2double((int)hi[1], (int)lo[1]);
     }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
+    // the lane index, recomputed (volatile: the compiler cannot hoist it or values derived
+    // from it out of the solver's loops)
+    __device__ __forceinline__ int lane() const {
+        int r;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+        return r;
+    }
     __device__ __forceinline__ int uni(int v) const { return __builtin_amdgcn_readfirstlane(v); }
     // scheduling barrier: instructions are not moved across it (no wait is inserted)
     __device__ __forceinline__ void sched_fence() const { __builtin_amdgcn_sched_barrier(0); }

@@ -326,6 +326,7 @@ struct WideSolver {
     }
 
     MPCG_HD void stats(bool acc, T alpha, T amax_z) {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         wv.sync();
         if (acc) {
             // element-parallel: element e = 8k + j of the stage-major arrays, 64 per round
@@ -474,6 +475,7 @@ struct WideSolver {
     // ------------------------------------------------------- Riccati backward
     // Stage data that does not depend on the cost-to-go, all stages in parallel.
     MPCG_HD void precompute(int mode, T delta_w) {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         if (t >= N) return;
         const int k = t;
         const bool last = k == N - 1;
@@ -586,6 +588,7 @@ struct WideSolver {
     // stage: the forward pass needs only the gains, and the multipliers come from the
     // adjoint recursion (forward()).
     MPCG_HD bool riccati(int mode, T delta_w) {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         wv.sync();
         precompute(mode, delta_w);
         typedef WideLayout W_;
@@ -763,6 +766,7 @@ struct WideSolver {
     // theta, v), the upper 4..7 (cte, etheta, w, a); same per-variable formulas as the
     // unsplit sweep below (gradient of the barrier function, dir_var).
     MPCG_HD void step_stats_split(int k, const T* xk, const T* duk, Fwd& F) const {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         const bool hi = t >= 32, last = k == N - 1;
         const int j0 = hi ? 4 : 0;
         T w[4], zl[4], zu[4];
@@ -800,6 +804,7 @@ struct WideSolver {
     }
 
     MPCG_HD Fwd forward(int mode) {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         wv.sync();
         // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
         // systolically: lane k holds stage k's records, every step every lane applies its
@@ -980,6 +985,7 @@ struct WideSolver {
 
     // ------------------------------------------------------------ trial point
     MPCG_HD bool trial(T alpha, T* phi, T* th) {
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         T f = 0, thv = 0, lg = 0;
         int bad = 0;
         T Fk[6] = {0, 0, 0, 0, 0, 0};

@@ -50,6 +50,7 @@ struct HostWave {
         return r != 0;
     }
     int uni(int v) const { return v; }
+    int lane() const { return t; }
     void mark(int) const {}
     void sched_fence() const {}
     void ld2(int i, double& a, double& b) const {
