@@ -325,8 +325,9 @@ struct WideSolver {
         *zun = tmax(tmin(b, ksig * mu * ru2), mu * ru2 * iksig);
     }
 
-    MPCG_HD void stats(bool acc, T alpha, T amax_z) {
-        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
+    // Accept the step (w, z_L, z_U with the step lengths, y towards y+): element-parallel
+    // over the 8N entries of the stage-major arrays, 64 per round.
+    MPCG_HD void accept_all(int t, bool acc, T alpha, T amax_z) {
         wv.sync();
         if (acc) {
             // element-parallel: element e = 8k + j of the stage-major arrays, 64 per round
@@ -352,6 +353,182 @@ struct WideSolver {
             }
         }
         wv.sync();
+    }
+
+    // Statistics of the iterate (SPLIT): lane k of the lower half-wave takes stage k's
+    // variables 0..3, dynamics rows 0..3 and the heading theta, lane 32 + k the variables
+    // 4..7, rows 4, 5 and the heading error; the one Jacobian entry the lower half needs
+    // from the upper (d cte+ / d v = sin(etheta) dt) crosses by v_permlane32_swap.  Same
+    // per-quantity formulas as the unsplit sweep (stats()); the stage-table entries are
+    // written by the half-wave that computes them.
+    MPCG_HD void stats_split(bool acc, T alpha, T amax_z) {
+        const int t = wv.lane();
+        accept_all(t, acc, alpha, amax_z);
+        const int k = t & 31;
+        const bool hi = t >= 32, act = k < N, last = k == N - 1;
+        const int j0 = hi ? 4 : 0, nr = hi ? 2 : 4;
+        T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
+          lg = 0;
+        T Fa[4] = {0, 0, 0, 0}, A[4] = {0, 0, 0, 0};
+        T w[8], zl[4], zu[4], yq[4], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0};
+        T twk = dt, tvk = 0, f1 = 0;
+        if (act) {
+            ldn<8>(L.W(k), w);
+            ldv<4>(L.ZL(k) + j0, zl);
+            ldv<4>(L.ZU(k) + j0, zu);
+            ldv<4>(L.Y(k) + j0, yq);  // (upper half: y4, y5 and two unused entries)
+            const int sb = L.ST(k);
+            T cv[3] = {0, 0, 0};
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                up[0] = ld(L.W(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7);
+                T sa, ca;
+                sc_t(hi ? w[5] : w[2], &sa, &ca);
+                const T x = w[0], v = w[3];
+                const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
+                f1 = pr.c[1] + (T)2 * pr.c[2] * x + (T)3 * pr.c[3] * x * x;
+                const T f2 = (T)2 * pr.c[2] + (T)6 * pr.c[3] * x;
+                // Lin::jac: lower a0..a3 (x, y rows), upper a4..a6 (cte row)
+                A[0] = hi ? f1 : -w[3] * sa * dt;
+                A[1] = hi ? sa * dt : ca * dt;
+                A[2] = w[3] * ca * dt;
+                A[3] = sa * dt;
+                // next_m: lower rows 0..3, upper rows 4, 5
+                T turn = w[6] * dt;
+                if (model == 1) turn = w[3] * w[6] / lf * dt;
+                Fa[0] = (hi ? fx - w[1] : w[0]) + w[3] * (hi ? sa : ca) * dt;
+                Fa[1] = hi ? (model == 1 ? w[5] + turn : w[5] + w[6] * dt) : w[1] + w[3] * sa * dt;
+                Fa[2] = model == 1 ? w[2] + turn : w[2] + w[6] * dt;
+                Fa[3] = w[3] + w[7] * dt;
+                turn_d(w, w + 6, &twk, &tvk);
+                // constraint curvature: lower Q22 Q32, upper Q00 Q55 Q53
+                cv[0] = hi ? -yn[4] * f2 : yn[0] * v * ca * dt + yn[1] * v * sa * dt;
+                cv[1] = hi ? yn[4] * v * sa * dt : yn[0] * sa * dt - yn[1] * ca * dt;
+                cv[2] = -yn[4] * ca * dt;
+                T wn[4];
+                ldv<4>(L.W(k + 1) + j0, wn);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q < nr) st(sb + WideLayout::SD + j0 + q, Fa[q] - wn[q]);
+            }
+            const int na = hi ? 3 : 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < na) st(sb + WideLayout::SA + j0 + q, A[q]);
+            if (hi) {
+                st(sb + WideLayout::SCV + 0, cv[0]);
+                st(sb + WideLayout::SCV + 3, cv[1]);
+                st(sb + WideLayout::SCV + 4, cv[2]);
+            } else {
+                st(sb + WideLayout::SCV + 1, cv[0]);
+                st(sb + WideLayout::SCV + 2, cv[1]);
+            }
+            if constexpr (MODEL == 1) {
+                if (!hi) {
+                    st(sb + WideLayout::STW, twk);
+                    st(sb + WideLayout::STV, tvk);
+                    st(sb + WideLayout::SHVD, last ? (T)0 : -(yn[2] + yn[5]) / lf * dt);
+                }
+            }
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+        }
+        // d cte+ / d v of the upper half-wave for the lower half's (A^T yn)[3]
+        T a5own, a5;
+        wv.xor32_pair(A[1], a5own, a5);
+        T Fprev[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Fprev[q] = wv.up1(Fa[q]);
+        if (act) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < nr) {
+                    const int j = j0 + q;
+                    const T wj = hi ? w[4 + q] : w[q];
+                    const T c = k == 0 ? wj - (hi ? pr.init[4 + q] : pr.init[q]) : wj - Fprev[q];
+                    const T rsc = rowscale(j, k);
+                    const T cs = rsc * c;
+                    th += fabs(cs);
+                    pinf = tmax(pinf, (T)fabs(cs));
+                    puns = tmax(puns, (T)fabs(c));
+                    ly += fabs(yq[q]) * rcp(rsc);
+                }
+            }
+            const T e1 = w[4] - (T)P.ref_cte, e2 = w[5] - (T)P.ref_eth, e3 = w[3] - (T)P.ref_v;
+            T fu = (T)P.w_cte * e1 * e1 + (T)P.w_eth * e2 * e2;
+            // gradient of the Lagrangian's constraint part, A^T yn (AT_mul) and B^T yn
+            T at[4] = {0, 0, 0, 0}, gu[2] = {0, 0};
+            if (!last) {
+                if (hi) {
+                    at[1] = A[2] * yn[4] + yn[5];  // (A^T yn)[5] = a6 yn4 + yn5
+                } else {
+                    at[0] = yn[0] + f1 * yn[4];
+                    at[1] = yn[1] - yn[4];
+                    at[2] = A[0] * yn[0] + A[2] * yn[1] + yn[2];
+                    at[3] = A[1] * yn[0] + A[3] * yn[1] + yn[3] + a5 * yn[4];
+                    if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
+                }
+                grad_ctrl(k, um, w + 6, up, gu);
+                fu += cost_ctrl(k, w + 6, up);
+            }
+            f = hi ? fu : (T)P.w_v * e3 * e3;
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
+            // the objective gradient of this half's variables (scaled): g3 / g4, g5, gu
+            const T g3 = (T)(2.0 * P.w_v) * (w[3] - (T)P.ref_v);
+            const T g4 = (T)(2.0 * P.w_cte) * (w[4] - (T)P.ref_cte), g5 = (T)(2.0 * P.w_eth) * (w[5] - (T)P.ref_eth);
+            const int nv = (last && hi) ? 2 : 4;
+            T slackprod = 1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < nv) {
+                    const T wq = hi ? w[4 + q] : w[q];
+                    T gj;
+                    if (q < 2)
+                        gj = hi ? sf * (q == 0 ? g4 : g5) + yq[q] - at[q] : sf * (T)0 + yq[q] - at[q];
+                    else
+                        gj = hi ? sf * gu[q - 2] - (q == 2 ? btw : bta) : (q == 2 ? sf * (T)0 : sf * g3) + yq[q] - at[q];
+                    const T rd = gj - zl[q] + zu[q];
+                    dinf = tmax(dinf, (T)fabs(rd));
+                    const T lo = q < 2 ? sl : (q == 2 ? (hi ? wl : sl) : (hi ? al : sl));
+                    const T hb = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
+                    const T dl = wq - lo, du = hb - wq;
+                    slackprod *= dl * du;
+                    const T p1 = dl * zl[q], p2 = du * zu[q];
+                    c0 = tmax(c0, tmax((T)fabs(p1), (T)fabs(p2)));
+                    mn = tmin(mn, tmin(p1, p2));
+                    mx = tmax(mx, tmax(p1, p2));
+                    lz += fabs(zl[q]) + fabs(zu[q]);
+                }
+            }
+            lg = log(slackprod);
+        }
+        T v[11] = {f, th, pinf, puns, dinf, c0, mn, mx, ly, lz, lg};
+        const int op[11] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM};
+        reduce<11, true>(v, op);
+        fval = v[0];
+        theta = v[1];
+        prim_inf = v[2];
+        prim_uns = v[3];
+        dual_inf = v[4];
+        compl0 = v[5];
+        pmin = v[6];
+        pmax = v[7];
+        l1y = v[8];
+        l1z = v[9];
+        logsum = v[10];
+        wv.mark(0);
+    }
+
+    MPCG_HD void stats(bool acc, T alpha, T amax_z) {
+        if constexpr (SPLIT) {
+            stats_split(acc, alpha, amax_z);
+            return;
+        }
+        const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
+        accept_all(t, acc, alpha, amax_z);
         T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
           lg = 0;
         T Fk[6] = {0, 0, 0, 0, 0, 0};
@@ -745,21 +922,17 @@ struct WideSolver {
 
     // Lane masks of the systolic recursions (bit t: lane t keeps its vector this step):
     // stages k <= s (step recursion) / k >= s (multiplier recursion), in both half-waves
-    // when SPLIT.
-    MPCG_HD unsigned long long keep_up(int s) const {
-        if constexpr (SPLIT) {
-            const unsigned long long m = s >= 31 ? 0xFFFFFFFFull : ((2ull << s) - 1);
-            return m | (m << 32);
-        } else {
-            return s >= 63 ? ~0ull : ((2ull << s) - 1);
-        }
-    }
+    // when SPLIT.  Carried from step to step (two or three scalar operations per step):
+    //   up: m_s = (m_{s-1} << 1) | UP1, m_{-1} = 0;  down: m_s = ((m_{s+1} >> 1) & DNM) | DNT.
+    static constexpr unsigned long long UP1 = SPLIT ? 0x0000000100000001ull : 1ull;
+    static constexpr unsigned long long DNM = SPLIT ? 0x7FFFFFFF7FFFFFFFull : 0x7FFFFFFFFFFFFFFFull;
+    static constexpr unsigned long long DNT = SPLIT ? 0x8000000080000000ull : 0x8000000000000000ull;
     MPCG_HD unsigned long long keep_dn(int s) const {
         if constexpr (SPLIT) {
             const unsigned long long m = (0xFFFFFFFFull << s) & 0xFFFFFFFFull;
             return m | (m << 32);
         } else {
-            return ~0ull << s;
+            return s >= 64 ? 0ull : (~0ull << s);
         }
     }
     // Step statistics of stage k (SPLIT): the lower half-wave takes variables 0..3 (x, y,
@@ -844,6 +1017,7 @@ struct WideSolver {
         // writes only lanes above the current step), so after the last step every lane
         // holds its own stage's step and, recomputed from it, its control step.
         T du0 = 0, du1 = 0;
+        unsigned long long mk = 0;
         for (int s = 0; s < N; ++s) {
             T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
 #pragma unroll
@@ -868,7 +1042,8 @@ struct WideSolver {
             for (int j = 0; j < 6; ++j) y[j] += d[j];
             y[6] = du0;
             y[7] = du1;
-            wv.up8_keep(x, y, keep_up(s));
+            mk = (mk << 1) | UP1;
+            wv.up8_keep(x, y, mk);
         }
         const T* xk = x;
         const T duk[2] = {du0, du1};
@@ -920,12 +1095,14 @@ struct WideSolver {
         // (as the step recursion: lane k keeps its multiplier input from step k on, so the
         // last step's output in lane k is stage k's)
         T o[6];
+        unsigned long long md = keep_dn(N);
         for (int s = N - 1; s >= 0; --s) {
             AT_mul(ak, lam, o);
             if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) o[q] += base[q];
-            wv.dn6_keep(lam, o, keep_dn(s));
+            md = ((md >> 1) & DNM) | DNT;
+            wv.dn6_keep(lam, o, md);
         }
         if (t < N) {
 #pragma unroll
@@ -984,7 +1161,92 @@ struct WideSolver {
     }
 
     // ------------------------------------------------------------ trial point
+    // Trial point (SPLIT): lane k of the lower half-wave takes stage k's variables 0..3,
+    // the heading theta and dynamics rows 0..3, lane 32 + k the variables 4..7, the
+    // heading error and rows 4, 5: one sine/cosine and half the slacks per lane.  Same
+    // per-quantity formulas as the unsplit sweep (trial()).
+    MPCG_HD bool trial_split(T alpha, T* phi, T* th) {
+        const int t = wv.lane();
+        const int k = t & 31;
+        const bool hi = t >= 32, act = k < N, last = k == N - 1;
+        T f = 0, thv = 0, lg = 0;
+        int bad = 0;
+        T Fa[4] = {0, 0, 0, 0};
+        T w[8];
+        if (act) {
+            T cw[8], cd[8];
+            ldn<8>(L.W(k), cw);
+            ldn<8>(L.DW(k), cd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = cw[j] + alpha * cd[j];
+            const int nv = (last && hi) ? 2 : 4;
+            T slackprod = 1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < nv) {
+                    const T wq = hi ? w[4 + q] : w[q];
+                    const T lo = q < 2 ? sl : (q == 2 ? (hi ? wl : sl) : (hi ? al : sl));
+                    const T up_ = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
+                    const T dl = wq - lo, du = up_ - wq;
+                    bad |= !((dl > 0) && (du > 0));
+                    slackprod *= dl * du;
+                }
+            }
+            lg = log(slackprod);
+            // objective: v term (lower), cte / etheta terms and the controls (upper)
+            const T e1 = w[4] - (T)P.ref_cte, e2 = w[5] - (T)P.ref_eth, e3 = w[3] - (T)P.ref_v;
+            T fu = (T)P.w_cte * e1 * e1 + (T)P.w_eth * e2 * e2;
+            if (!last) {
+                T up[2];
+                up[0] = ld(L.W(k + 1) + 6) + alpha * ld(L.DW(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7) + alpha * ld(L.DW(k + 1) + 7);
+                fu += cost_ctrl(k, w + 6, up);
+            }
+            f = hi ? fu : (T)P.w_v * e3 * e3;
+            if (!last) {
+                // (Lin::eval / Lin::next / next_m, one angle per half-wave)
+                T sa, ca;
+                sc_t(hi ? w[5] : w[2], &sa, &ca);
+                const T x = w[0];
+                const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
+                T turn = w[6] * dt;
+                if (model == 1) turn = w[3] * w[6] / lf * dt;
+                Fa[0] = (hi ? fx - w[1] : w[0]) + w[3] * (hi ? sa : ca) * dt;
+                Fa[1] = hi ? (model == 1 ? w[5] + turn : w[5] + w[6] * dt) : w[1] + w[3] * sa * dt;
+                Fa[2] = model == 1 ? w[2] + turn : w[2] + w[6] * dt;
+                Fa[3] = w[3] + w[7] * dt;
+            }
+        }
+        T Fprev[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Fprev[q] = wv.up1(Fa[q]);
+        if (act) {
+            const int nr = hi ? 2 : 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < nr) {
+                    const int j = hi ? 4 + q : q;
+                    const T wj = hi ? w[4 + q] : w[q];
+                    const T c = k == 0 ? wj - (hi ? pr.init[4 + q] : pr.init[q]) : wj - Fprev[q];
+                    thv += fabs(rowscale(j, k) * c);
+                }
+            }
+        }
+        T v[3] = {f, thv, lg};
+        const int op[3] = {RSUM, RSUM, RSUM};
+        reduce<3, true>(v, op);
+        f = v[0];
+        thv = v[1];
+        lg = v[2];
+        const bool anybad = wv.any(bad != 0);
+        wv.mark(6);
+        *phi = sf * f - mu * lg;
+        *th = thv;
+        return !anybad && isfinite((double)*phi);
+    }
+
     MPCG_HD bool trial(T alpha, T* phi, T* th) {
+        if constexpr (SPLIT) return trial_split(alpha, phi, th);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         T f = 0, thv = 0, lg = 0;
         int bad = 0;

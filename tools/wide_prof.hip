@@ -26,10 +26,14 @@ const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj"
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
+    unsigned int* cnt;  // calls per phase mark
     unsigned long long last;
     __device__ void mark(int id) {
         const unsigned long long now = clock64();
-        if (t == 0) acc[id] += now - last;
+        if (t == 0) {
+            acc[id] += now - last;
+            cnt[id] += 1;
+        }
         last = now;
     }
 };
@@ -39,7 +43,7 @@ struct ProfWave : DevWaveBase {
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_prof(IpmParams P, int64_t B, const double* state, const double* coeffs,
                                              unsigned long long* acc, int* iters, int* status,
-                                             unsigned long long* times) {
+                                             unsigned long long* times, unsigned int* cnt) {
     const int64_t p = blockIdx.x;
     if (p >= B) return;
     IpmProblem<double> pr;
@@ -48,6 +52,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     ProfWave wv;
     wv.t = (int)threadIdx.x;
     wv.acc = acc + p * (NPH + 1);
+    wv.cnt = cnt + p * NPH;
     wv.last = (unsigned long long)clock64();
     const unsigned long long t0 = wv.last;
     const unsigned long long r0 = wall_clock64();
@@ -99,6 +104,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dss, B * 4));
     unsigned long long* dtm;
     CK(hipMalloc(&dtm, B * 16));
+    unsigned int* dcnt;
+    CK(hipMalloc(&dcnt, B * mpcg::NPH * 4));
+    CK(hipMemset(dcnt, 0, B * mpcg::NPH * 4));
     CK(hipMemcpy(dst, st.data(), B * 6 * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dcf, cf.data(), B * 4 * 8, hipMemcpyHostToDevice));
     CK(hipMemset(dacc, 0, B * W * 8));
@@ -108,7 +116,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss, dtm);
+    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss, dtm, dcnt);
     CK(hipGetLastError());
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
@@ -119,15 +127,18 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(acc.data(), dacc, B * W * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(it.data(), dit, B * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(ss.data(), dss, B * 4, hipMemcpyDeviceToHost));
-    double sum[W] = {0}, iters = 0;
+    std::vector<unsigned int> cn(B * mpcg::NPH);
+    CK(hipMemcpy(cn.data(), dcnt, B * mpcg::NPH * 4, hipMemcpyDeviceToHost));
+    double sum[W] = {0}, iters = 0, calls[W] = {0};
     for (int64_t p = 0; p < B; ++p) {
         for (int j = 0; j < W; ++j) sum[j] += (double)acc[p * W + j];
+        for (int j = 0; j < mpcg::NPH; ++j) calls[j] += cn[p * mpcg::NPH + j];
         iters += it[p];
     }
     std::printf("B=%lld kernel %.3f ms  iters/solve %.2f  lds %zu B\n", (long long)B, ms, iters / B, lds);
     for (int j = 0; j < mpcg::NPH; ++j)
-        std::printf("  %-10s %10.0f cyc/solve %8.0f cyc/iter  %5.1f%%\n", mpcg::kPhase[j], sum[j] / B, sum[j] / iters,
-                    100.0 * sum[j] / sum[mpcg::NPH]);
+        std::printf("  %-10s %10.0f cyc/solve %8.0f cyc/iter  %5.1f%%  %8.0f cyc/call\n", mpcg::kPhase[j], sum[j] / B,
+                    sum[j] / iters, 100.0 * sum[j] / sum[mpcg::NPH], calls[j] > 0 ? sum[j] / calls[j] : 0.0);
     std::printf("  %-10s %10.0f cyc/solve %8.0f cyc/iter\n", "total", sum[mpcg::NPH] / B, sum[mpcg::NPH] / iters);
     // dispatch timeline (wall_clock64 ticks, 100 MHz): when problems start and end
     std::vector<unsigned long long> tm(2 * B);
