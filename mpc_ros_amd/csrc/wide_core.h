@@ -56,7 +56,7 @@ struct WideLayout {
     static constexpr int SQD = 16;  // diag of the stage Hessian (6 states, 2 controls = R)
     static constexpr int SQV = 24;  // gradient q (6) and r (2)
     static constexpr int SCV = 32;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
-    static constexpr int SCC = 37;  // rate coupling C0 C1
+    static constexpr int SCC = 37;  // (unused: the rate coupling is a per-lane constant of the sweep)
     static constexpr int SZERO = 39, SONE = 40, SMONE = 41;  // constants 0, 1, -1
     // bicycle only: model terms of the heading rows (th, eth): d(turn)/d(w) (B_hat
     // column w: v/lf dt; dt for the differential drive), d(turn)/d(v) (A_hat column v:
@@ -704,7 +704,7 @@ struct WideSolver {
             st(sb + WideLayout::SQD + j, qd);
             st(sb + WideLayout::SQV + j, qv);
         }
-        T R[2] = {0, 0}, r[2] = {0, 0}, C0 = 0, C1 = 0;
+        T R[2] = {0, 0}, r[2] = {0, 0};
         if (!last) {
             T um[2] = {0, 0}, up[2], gu[2];
             if (k >= 1) {
@@ -725,17 +725,11 @@ struct WideSolver {
                     r[j] = sf * gu[j] - zl[6 + j] + zu[6 + j];
                 }
             }
-            if (mode == 0 && k >= 1) {
-                C0 = -sf * (T)(2.0 * P.w_dw);
-                C1 = -sf * (T)(2.0 * P.w_da);
-            }
         }
         st(sb + WideLayout::SQD + 6, R[0]);
         st(sb + WideLayout::SQD + 7, R[1]);
         st(sb + WideLayout::SQV + 6, r[0]);
         st(sb + WideLayout::SQV + 7, r[1]);
-        st(sb + WideLayout::SCC + 0, C0);
-        st(sb + WideLayout::SCC + 1, C1);
     }
 
     // Stage-table offset of G[m][s], G = [A_hat cols 0,1,2,3,5 | B_hat cols w,a | d]
@@ -781,9 +775,18 @@ struct WideSolver {
         const bool hj = sj >= 0, hi = si >= 0;
         const int gj = sm + MS * j, mi = hi ? sm + MS * si : L.ZB(), mj = hj ? sm + MS * sj : L.ZB();
         const int gsrc = goff(i, j);
-        // the rate-coupling entries of S_tilde
-        const int c0j = j == 6 ? W_::SCC : W_::SZERO, c1j = j == 7 ? W_::SCC + 1 : W_::SZERO;
-        const int c0i = i == 6 ? W_::SCC : W_::SZERO, c1i = i == 7 ? W_::SCC + 1 : W_::SZERO;
+        // the rate-coupling entries of S_tilde: -sf 2 W_DANGVEL / -sf 2 W_DA on the previous
+        // control's columns, the same for every stage (the Newton system, mode 0).  Stage 0
+        // has no previous control: its coupling entries act only on K_0's columns 6, 7, which
+        // multiply a zero step, and on P_0, which is not used.
+        const T C0 = mode == 0 ? -sf * (T)(2.0 * P.w_dw) : (T)0, C1 = mode == 0 ? -sf * (T)(2.0 * P.w_da) : (T)0;
+        const T cc0j = j == 6 ? C0 : (T)0, cc1j = j == 7 ? C1 : (T)0;
+        const T cc0i = i == 6 ? C0 : (T)0, cc1i = i == 7 ? C1 : (T)0;
+        // the gains' store at ga0 + gak * k: lanes 0..15 K[0][j], K[1][j], lanes 16, 17 k;
+        // the other lanes store into their own slot of the G staging, which they
+        // overwrite right after
+        const int ga0 = t < 16 ? L.KR(0) + t : (t < 18 ? L.ST(0) + W_::SKF + (t - 16) : sm + MS * i + j);
+        const int gak = t < 16 ? WideLayout::KS : (t < 18 ? L.SS : 0);
         // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
         const int hvj = j == 3 ? W_::SHVD : W_::SZERO, hvi = i == 3 ? W_::SHVD : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
@@ -811,16 +814,17 @@ struct WideSolver {
             const int sb = L.ST(k);
             // row i of P' (16-byte reads of the scratch the previous stage wrote) and all
             // P-independent stage data, issued together before anything waits on them
-            T pr_[8], g[8], c[8];
+            T pr_[8], g[8], c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             wv.sync();
             ldv<8>(sp + 8 * i, pr_);
             ldv<8>(gj, g);
-            ldv<8>(mi, c);
+            // A_hat column i: rows 0..5 (rows 6, 7 are zero; the differential drive's own
+            // entry is row i itself, the bicycle's heading-rate terms rows 2 and 5)
+            ldv<6>(mi, c);
             const T gnext = ld(L.ST(k > 0 ? k - 1 : 0) + gsrc);  // next stage's G entry
             T qd6, qd7, qv6, qv7;
             ld2(sb + W_::SQD + 6, qd6, qd7);
             ld2(sb + W_::SQV + 6, qv6, qv7);
-            const T cc0j = ld(sb + c0j), cc1j = ld(sb + c1j), cc0i = ld(sb + c0i), cc1i = ld(sb + c1i);
             const T qh1 = ld(sb + q1), qh2 = ld(sb + q2);
             const T qvi = ld(sb + qv);
             T hv0j = 0, hv0i = 0;
@@ -876,7 +880,7 @@ struct WideSolver {
             // (A_hat^T M)(i, j) and (A_hat^T h)(i)
             T a0 = 0, a1 = 0, h0 = 0, h1 = 0;
 #pragma unroll
-            for (int q = 0; q < 8; q += 2) {
+            for (int q = 0; q < 6; q += 2) {
                 a0 += c[q] * mc[q];
                 a1 += c[q + 1] * mc[q + 1];
                 h0 += c[q] * m7[q];
@@ -886,12 +890,10 @@ struct WideSolver {
             Pij = qh + (a0 + a1) + s0i * K0 + s1i * K1;
             pvi = qvi + (h0 + h1) + s0i * kf0 + s1i * kf1;
             st(sp + t, Pij);
-            // gains K (lanes 0..15: K[0][j], K[1][j]) and k (lanes 16, 17) in one store
-            if (t < 18) {
-                const int a = t < 16 ? L.KR(k) + t : sb + W_::SKF + (t - 16);
-                st(a, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
-            }
             wv.sync();  // this stage's reads of M are done
+            // gains K (lanes 0..15: K[0][j], K[1][j]) and k (lanes 16, 17) in one store (the
+            // other lanes' store lands in the G slot the next store overwrites)
+            st(ga0 + gak * k, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
             st(sm + MS * i + j, gnext);
         }
         // a failed inertia test anywhere (the stages after it computed values the retry overwrites)
