@@ -10,3 +10,4 @@ run b16384 --batch 16384 --steps 5 --warmup 1
 run lane --strategy lane --steps 2 --warmup 1
 run track --mode track --steps 5 --warmup 1
 run b4096_cpu --batch 4096 --steps 10 --warmup 2 --cpu-seconds 10
+run bicycle_n25 --model bicycle --horizon 25 --steps 3 --warmup 1
