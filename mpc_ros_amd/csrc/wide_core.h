@@ -299,6 +299,13 @@ struct WideSolver {
     MPCG_HD void init_point() {
         if (t < N) {
             const int k = t;
+            // constant entries of the stage table (dt, 0, 1, -1: gather targets of the
+            // Riccati's per-lane offsets), written once
+            const int sb = L.ST(k);
+            st(sb + WideLayout::SDT, dt);
+            st(sb + WideLayout::SZERO, 0);
+            st(sb + WideLayout::SONE, 1);
+            st(sb + WideLayout::SMONE, -1);
             for (int j = 0; j < 8; ++j) {
                 st(L.W(k) + j, push((j < 6 && k == 0) ? pr.init[j] : (T)0, vlo(j), vhi(j)));
                 st(L.ZL(k) + j, 1);
@@ -651,7 +658,86 @@ struct WideSolver {
 
     // ------------------------------------------------------- Riccati backward
     // Stage data that does not depend on the cost-to-go, all stages in parallel.
+    // Stage data of the Newton system (SPLIT): the lower half-wave takes the barrier
+    // Hessian diagonal and gradient of stage k's variables 0..3, the upper of 4..7 (the
+    // controls' R and r); mode 1's linearisation stays with the lower half.  Same
+    // per-variable formulas as the unsplit sweep (precompute()).
+    MPCG_HD void precompute_split(int mode, T delta_w) {
+        const int t = wv.lane();
+        const int k = t & 31;
+        const bool hi = t >= 32;
+        if (k >= N) return;
+        const bool last = k == N - 1;
+        const int sb = L.ST(k);
+        if (mode == 1 && !hi) {
+            T w[8];
+            ldn<8>(L.W(k), w);
+            T a[7] = {0, 0, 0, 0, 0, 0, 0}, tw = dt, tv = 0;
+            if (!last) {
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                ln.jac(w, dt, a);
+                turn_d(w, w + 6, &tw, &tv);
+            }
+#pragma unroll
+            for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+            if constexpr (MODEL == 1) {
+                st(sb + WideLayout::STW, tw);
+                st(sb + WideLayout::STV, tv);
+                st(sb + WideLayout::SHVD, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, 0);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, 0);
+        }
+        const int j0 = hi ? 4 : 0;
+        T w[4], zl[4], zu[4];
+        ldv<4>(L.W(k) + j0, w);
+        ldv<4>(L.ZL(k) + j0, zl);
+        ldv<4>(L.ZU(k) + j0, zu);
+        T gu[2] = {0, 0};
+        if (!last) {
+            T um[2] = {0, 0}, up[2];
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            up[0] = ld(L.W(k + 1) + 6);
+            up[1] = ld(L.W(k + 1) + 7);
+            grad_ctrl(k, um, w + 2, up, gu);  // (upper half: w + 2 = variables 6, 7)
+        }
+        const T g3 = (T)(2.0 * P.w_v) * (w[3] - (T)P.ref_v);
+        const T g4 = (T)(2.0 * P.w_cte) * (w[0] - (T)P.ref_cte), g5 = (T)(2.0 * P.w_eth) * (w[1] - (T)P.ref_eth);
+        const int nv = (last && hi) ? 2 : 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            T qd = 0, qv = 0;
+            if (q < nv) {
+                const T gq = hi ? (q == 0 ? g4 : (q == 1 ? g5 : gu[q - 2])) : (q == 3 ? g3 : (T)0);
+                const T hq = hi ? (q < 2 ? hess_state(4 + q) : hess_ctrl(k, q - 2)) : hess_state(q);
+                const T lo = q < 2 ? sl : (q == 2 ? (hi ? wl : sl) : (hi ? al : sl));
+                const T hb = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
+                if (mode == 0) {
+                    const T rdl = rcp(w[q] - lo), rdu = rcp(hb - w[q]);
+                    qd = sf * hq + zl[q] * rdl + zu[q] * rdu + delta_w;
+                    qv = sf * gq - mu * rdl + mu * rdu;
+                } else {
+                    qd = 1;
+                    qv = sf * gq - zl[q] + zu[q];
+                }
+            }
+            // (the last stage's controls: R = r = 0)
+            st(sb + WideLayout::SQD + j0 + q, qd);
+            st(sb + WideLayout::SQV + j0 + q, qv);
+        }
+    }
+
     MPCG_HD void precompute(int mode, T delta_w) {
+        if constexpr (SPLIT) {
+            precompute_split(mode, delta_w);
+            return;
+        }
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         if (t >= N) return;
         const int k = t;
@@ -686,10 +772,6 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, 0);
         }
-        st(sb + WideLayout::SDT, dt);
-        st(sb + WideLayout::SZERO, 0);
-        st(sb + WideLayout::SONE, 1);
-        st(sb + WideLayout::SMONE, -1);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             T qd, qv;
