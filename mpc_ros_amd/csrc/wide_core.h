@@ -104,6 +104,11 @@ struct WideSolver {
     // line-search / iteration state
     T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt;
     int iter, nf, status;
+    // SPLIT: the sine/cosine pair of the last trial point (the lane's heading theta or
+    // etheta), which the next statistics sweep reuses when that trial point was
+    // accepted (the accepted iterate is bitwise the trial point: both are w + alpha dw)
+    T c_sa = 0, c_ca = 0;
+    int c_ok = 0;
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
@@ -371,10 +376,12 @@ struct WideSolver {
     MPCG_HD void stats_split(bool acc, T alpha, T amax_z) {
         const int t = wv.lane();
         accept_all(t, acc, alpha, amax_z);
+        const bool reuse = acc && c_ok;  // (uniform)
+        c_ok = 0;
         const int k = t & 31;
         const bool hi = t >= 32, act = k < N, last = k == N - 1;
         const int j0 = hi ? 4 : 0, nr = hi ? 2 : 4;
-        T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
+        T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
           lg = 0;
         T Fa[4] = {0, 0, 0, 0}, A[4] = {0, 0, 0, 0};
         T w[8], zl[4], zu[4], yq[4], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0};
@@ -391,7 +398,12 @@ struct WideSolver {
                 up[0] = ld(L.W(k + 1) + 6);
                 up[1] = ld(L.W(k + 1) + 7);
                 T sa, ca;
-                sc_t(hi ? w[5] : w[2], &sa, &ca);
+                if (reuse) {
+                    sa = c_sa;
+                    ca = c_ca;
+                } else {
+                    sc_t(hi ? w[5] : w[2], &sa, &ca);
+                }
                 const T x = w[0], v = w[3];
                 const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
                 f1 = pr.c[1] + (T)2 * pr.c[2] * x + (T)3 * pr.c[3] * x * x;
@@ -504,7 +516,6 @@ struct WideSolver {
                     const T dl = wq - lo, du = hb - wq;
                     slackprod *= dl * du;
                     const T p1 = dl * zl[q], p2 = du * zu[q];
-                    c0 = tmax(c0, tmax((T)fabs(p1), (T)fabs(p2)));
                     mn = tmin(mn, tmin(p1, p2));
                     mx = tmax(mx, tmax(p1, p2));
                     lz += fabs(zl[q]) + fabs(zu[q]);
@@ -512,20 +523,21 @@ struct WideSolver {
             }
             lg = log(slackprod);
         }
-        T v[11] = {f, th, pinf, puns, dinf, c0, mn, mx, ly, lz, lg};
-        const int op[11] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM};
-        reduce<11, true>(v, op);
+        // (max |z s| = max(max z s, -min z s): one reduction fewer)
+        T v[10] = {f, th, pinf, puns, dinf, mn, mx, ly, lz, lg};
+        const int op[10] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM};
+        reduce<10, true>(v, op);
         fval = v[0];
         theta = v[1];
         prim_inf = v[2];
         prim_uns = v[3];
         dual_inf = v[4];
-        compl0 = v[5];
-        pmin = v[6];
-        pmax = v[7];
-        l1y = v[8];
-        l1z = v[9];
-        logsum = v[10];
+        pmin = v[5];
+        pmax = v[6];
+        compl0 = wv.uni_d(tmax(pmax, -pmin));
+        l1y = v[7];
+        l1z = v[8];
+        logsum = v[9];
         wv.mark(0);
     }
 
@@ -1291,6 +1303,8 @@ struct WideSolver {
                 // (Lin::eval / Lin::next / next_m, one angle per half-wave)
                 T sa, ca;
                 sc_t(hi ? w[5] : w[2], &sa, &ca);
+                c_sa = sa;
+                c_ca = ca;
                 const T x = w[0];
                 const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
                 T turn = w[6] * dt;
@@ -1301,6 +1315,7 @@ struct WideSolver {
                 Fa[3] = w[3] + w[7] * dt;
             }
         }
+        c_ok = 1;
         T Fprev[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) Fprev[q] = wv.up1(Fa[q]);
@@ -1508,6 +1523,7 @@ struct WideSolver {
         T alpha = F.amax_p;
         bool accepted = false, ftype = false;
         const int fi = L.FI();
+        c_ok = 0;
         for (int ls = 0; ls < 60; ++ls) {
             if (wv.uni(tiny)) { accepted = true; ftype = true; break; }
             if (wv.uni(alpha < alpha_min)) break;
