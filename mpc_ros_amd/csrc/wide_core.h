@@ -109,6 +109,9 @@ struct WideSolver {
     // accepted (the accepted iterate is bitwise the trial point: both are w + alpha dw)
     T c_sa = 0, c_ca = 0;
     int c_ok = 0;
+    // SPLIT: reciprocal slacks 1/(w - lo), 1/(hi - w) of the lane's four variables, from
+    // the stage data of the Newton system (same iterate) to the step statistics
+    T c_rdl[4] = {0, 0, 0, 0}, c_rdu[4] = {0, 0, 0, 0};
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
@@ -732,6 +735,8 @@ struct WideSolver {
                 const T hb = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
                 if (mode == 0) {
                     const T rdl = rcp(w[q] - lo), rdu = rcp(hb - w[q]);
+                    c_rdl[q] = rdl;
+                    c_rdu[q] = rdu;
                     qd = sf * hq + zl[q] * rdl + zu[q] * rdu + delta_w;
                     qv = sf * gq - mu * rdl + mu * rdu;
                 } else {
@@ -1004,8 +1009,12 @@ struct WideSolver {
         T amax_p, amax_z, gd, rel;
     };
     MPCG_HD void dir_var(T w, T zl, T zu, T lo, T hi, T gphi, T dwv, Fwd& F) const {
+        dir_var_r(w, zl, zu, lo, hi, gphi, dwv, rcp(w - lo), rcp(hi - w), F);
+    }
+    // (with the reciprocal slacks rdl = rcp(w - lo), rdu = rcp(hi - w) given)
+    MPCG_HD void dir_var_r(T w, T zl, T zu, T lo, T hi, T gphi, T dwv, T rdl, T rdu, Fwd& F) const {
         const T dl = w - lo, du = hi - w;
-        const T rdl = rcp(dl), rdu = rcp(du), rdw = rcp(dwv);
+        const T rdw = rcp(dwv);
         const T inf = (T)INFINITY;
         F.amax_p = tmin(F.amax_p, dwv < 0 ? -tau * dl * rdw : (dwv > 0 ? tau * du * rdw : inf));
         const T dzl = mu * rdl - zl - zl * rdl * dwv;
@@ -1066,8 +1075,8 @@ struct WideSolver {
         for (int q = 0; q < 4; ++q) {
             if (q < nv) {
                 const T lo = q < 2 ? sl : (q == 2 ? lo2 : lo3), up_ = q < 2 ? su : (q == 2 ? hi2 : hi3);
-                const T gphi = gq[q] - mu * rcp(w[q] - lo) + mu * rcp(up_ - w[q]);
-                dir_var(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], F);
+                const T gphi = gq[q] - mu * c_rdl[q] + mu * c_rdu[q];
+                dir_var_r(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], c_rdl[q], c_rdu[q], F);
             }
         }
     }
