@@ -10,8 +10,9 @@
 //                   xor 16 (ds_swizzle), xor 32 (ds_bpermute).  Pairs are symmetric, so
 //                   a commutative op leaves every lane with identical bits;
 //   up1(v), dn1(v)  value of lane t-1 / t+1 (DPP wave_shr:1 / wave_shl:1; lanes 0 / 63: undefined);
-//   up8_keep(x, y, m), dn6_keep(x, y, m)  x := y of lane t-1 (t+1) except in the lanes of the
-//                   mask m, which keep x (the systolic recursions);
+//   up8(x, y), dn6(x, y)  x := y of lane t-1 (t+1); lane 0 (63) keeps x (the systolic
+//                   recursions);
+//   lo_half(v)      v of lane t & 31 (v_permlane32_swap);
 //   xor32_pair(v, a, b)  {a, b} = {v, v of lane t ^ 32} (v_permlane32_swap);
 //   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
 //   lane()          the lane index, recomputed by a volatile v_mbcnt pair: each solver phase
@@ -89,76 +90,29 @@ struct DevWaveBase {
     __device__ __forceinline__ double up1(double v) const { return dpp<0x138>(v); }
     // DPP wave_shl:1: lane t reads lane t+1
     __device__ __forceinline__ double dn1(double v) const { return dpp<0x130>(v); }
-    // keep ? old : up1(v) / dn1(v) (a select on the shifted value: one v_cndmask per dword)
-    // x[q] = (lane in keep) ? x[q] : y[q] of lane t-1 (UP) / t+1 (!UP), n doubles.
-    // One v_cndmask_b32_dpp per dword: the shift is the DPP modifier of the select's
-    // first source (the compiler emits a DPP move and a separate select).  keep is a lane
-    // mask (bit t: lane t keeps).  Two wait states separate the VALU writes of y from
-    // the DPP reads (s_mov + s_nop 1).
-    template <bool UP>
-    __device__ __forceinline__ static void shift4_keep(double* x, const double* y, unsigned long long keep) {
-        int xl0 = __double2loint(x[0]), xh0 = __double2hiint(x[0]), xl1 = __double2loint(x[1]),
-            xh1 = __double2hiint(x[1]), xl2 = __double2loint(x[2]), xh2 = __double2hiint(x[2]),
-            xl3 = __double2loint(x[3]), xh3 = __double2hiint(x[3]);
-#define MPCG_CND(d, s) "v_cndmask_b32_dpp " d ", " s ", " d ", vcc " MPCG_SH " row_mask:0xf bank_mask:0xf\n\t"
-#define MPCG_ASM4                                                                                              \
-    asm("s_mov_b64 vcc, %16\n\ts_nop 1\n\t" MPCG_CND("%0", "%8") MPCG_CND("%1", "%9") MPCG_CND("%2", "%10") \
-            MPCG_CND("%3", "%11") MPCG_CND("%4", "%12") MPCG_CND("%5", "%13") MPCG_CND("%6", "%14")           \
-                MPCG_CND("%7", "%15")                                                                          \
-        : "+v"(xl0), "+v"(xh0), "+v"(xl1), "+v"(xh1), "+v"(xl2), "+v"(xh2), "+v"(xl3), "+v"(xh3)              \
-        : "v"(__double2loint(y[0])), "v"(__double2hiint(y[0])), "v"(__double2loint(y[1])),                    \
-          "v"(__double2hiint(y[1])), "v"(__double2loint(y[2])), "v"(__double2hiint(y[2])),                    \
-          "v"(__double2loint(y[3])), "v"(__double2hiint(y[3])), "s"(keep)                                     \
-        : "vcc")
-        if constexpr (UP) {
-#define MPCG_SH "wave_shr:1"
-            MPCG_ASM4;
-#undef MPCG_SH
-        } else {
-#define MPCG_SH "wave_shl:1"
-            MPCG_ASM4;
-#undef MPCG_SH
+    // x[q] := y[q] of lane t-1 (UP: DPP wave_shr:1) / t+1 (wave_shl:1), n doubles.  Lane 0
+    // (63), whose source lane does not exist, keeps x[q]: the DPP move with bound_ctrl off
+    // does not write it.  One v_mov_b32_dpp per dword, the old value tied to the result.
+    template <bool UP, int n>
+    __device__ __forceinline__ static void shift(double* x, const double* y) {
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int lo = __builtin_amdgcn_update_dpp(__double2loint(x[q]), __double2loint(y[q]),
+                                                       UP ? 0x138 : 0x130, 0xF, 0xF, false);
+            const int hi = __builtin_amdgcn_update_dpp(__double2hiint(x[q]), __double2hiint(y[q]),
+                                                       UP ? 0x138 : 0x130, 0xF, 0xF, false);
+            x[q] = __hiloint2double(hi, lo);
         }
-#undef MPCG_ASM4
-        x[0] = __hiloint2double(xh0, xl0);
-        x[1] = __hiloint2double(xh1, xl1);
-        x[2] = __hiloint2double(xh2, xl2);
-        x[3] = __hiloint2double(xh3, xl3);
     }
-    template <bool UP>
-    __device__ __forceinline__ static void shift2_keep(double* x, const double* y, unsigned long long keep) {
-        int xl0 = __double2loint(x[0]), xh0 = __double2hiint(x[0]), xl1 = __double2loint(x[1]),
-            xh1 = __double2hiint(x[1]);
-#define MPCG_ASM2                                                                                        \
-    asm("s_mov_b64 vcc, %8\n\ts_nop 1\n\t" MPCG_CND("%0", "%4") MPCG_CND("%1", "%5") MPCG_CND("%2", "%6") \
-            MPCG_CND("%3", "%7")                                                                         \
-        : "+v"(xl0), "+v"(xh0), "+v"(xl1), "+v"(xh1)                                                    \
-        : "v"(__double2loint(y[0])), "v"(__double2hiint(y[0])), "v"(__double2loint(y[1])),              \
-          "v"(__double2hiint(y[1])), "s"(keep)                                                          \
-        : "vcc")
-        if constexpr (UP) {
-#define MPCG_SH "wave_shr:1"
-            MPCG_ASM2;
-#undef MPCG_SH
-        } else {
-#define MPCG_SH "wave_shl:1"
-            MPCG_ASM2;
-#undef MPCG_SH
-        }
-#undef MPCG_ASM2
-#undef MPCG_CND
-        x[0] = __hiloint2double(xh0, xl0);
-        x[1] = __hiloint2double(xh1, xl1);
-    }
-    // the step recursion: lanes in keep keep their vector, the others take lane t-1's
-    __device__ __forceinline__ void up8_keep(double* x, const double* y, unsigned long long keep) const {
-        shift4_keep<true>(x, y, keep);
-        shift4_keep<true>(x + 4, y + 4, keep);
-    }
-    // the multiplier recursion: lanes in keep keep, the others take lane t+1's (6 doubles)
-    __device__ __forceinline__ void dn6_keep(double* x, const double* y, unsigned long long keep) const {
-        shift4_keep<false>(x, y, keep);
-        shift2_keep<false>(x + 4, y + 4, keep);
+    // the step recursion (8 doubles up) and the multiplier recursion (6 doubles down)
+    __device__ __forceinline__ void up8(double* x, const double* y) const { shift<true, 8>(x, y); }
+    __device__ __forceinline__ void dn6(double* x, const double* y) const { shift<false, 6>(x, y); }
+    // v of lane t & 31: the lower half-wave's value in both halves (v_permlane32_swap of v
+    // with itself moves the lower half into the upper)
+    __device__ __forceinline__ double lo_half(double v) const {
+        const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+        return __hiloint2double((int)hi[0], (int)lo[0]);
     }
     // {a, b} = {v, v of lane t ^ 32} in some order (v_permlane32_swap per dword: the lower
     // half-wave receives the upper half's values and vice versa)

@@ -1025,21 +1025,6 @@ struct WideSolver {
         F.rel = tmax(F.rel, (T)fabs(dwv) * rcp((T)1 + (T)fabs(w)));
     }
 
-    // Lane masks of the systolic recursions (bit t: lane t keeps its vector this step):
-    // stages k <= s (step recursion) / k >= s (multiplier recursion), in both half-waves
-    // when SPLIT.  Carried from step to step (two or three scalar operations per step):
-    //   up: m_s = (m_{s-1} << 1) | UP1, m_{-1} = 0;  down: m_s = ((m_{s+1} >> 1) & DNM) | DNT.
-    static constexpr unsigned long long UP1 = SPLIT ? 0x0000000100000001ull : 1ull;
-    static constexpr unsigned long long DNM = SPLIT ? 0x7FFFFFFF7FFFFFFFull : 0x7FFFFFFFFFFFFFFFull;
-    static constexpr unsigned long long DNT = SPLIT ? 0x8000000080000000ull : 0x8000000000000000ull;
-    MPCG_HD unsigned long long keep_dn(int s) const {
-        if constexpr (SPLIT) {
-            const unsigned long long m = (0xFFFFFFFFull << s) & 0xFFFFFFFFull;
-            return m | (m << 32);
-        } else {
-            return s >= 64 ? 0ull : (~0ull << s);
-        }
-    }
     // Step statistics of stage k (SPLIT): the lower half-wave takes variables 0..3 (x, y,
     // theta, v), the upper 4..7 (cte, etheta, w, a); same per-variable formulas as the
     // unsplit sweep below (gradient of the barrier function, dir_var).
@@ -1086,8 +1071,12 @@ struct WideSolver {
         wv.sync();
         // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
         // systolically: lane k holds stage k's records, every step every lane applies its
-        // own stage map to the vector it holds and passes the result one lane up, so lane
-        // k sees its correct input at step k (and keeps it).
+        // own stage map to the vector it holds and passes the result one lane up.  Lane 0
+        // keeps its input (no lane below it); after step s lanes 0..s+1 hold their correct
+        // inputs, and a lane whose input is correct recomputes the same output (bitwise)
+        // at every later step, so nothing needs masking.  (SPLIT: the recursion is correct
+        // in the lower half-wave; lane 32 takes lane 31's output, so the upper half's
+        // values are replaced by the lower half's after the loop.)
         const int ks = SPLIT ? (t & 31) : t;  // the lane's stage
         T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
         if (ks < N - 1) {
@@ -1118,11 +1107,9 @@ struct WideSolver {
             x[6] = 0;
             x[7] = 0;
         }
-        // Lane k's input is correct at step k; from then on the lane keeps it (the shift
-        // writes only lanes above the current step), so after the last step every lane
-        // holds its own stage's step and, recomputed from it, its control step.
+        // after the last step every lane k < N holds its own stage's step and, recomputed
+        // from it, its control step
         T du0 = 0, du1 = 0;
-        unsigned long long mk = 0;
         for (int s = 0; s < N; ++s) {
             T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
 #pragma unroll
@@ -1147,8 +1134,14 @@ struct WideSolver {
             for (int j = 0; j < 6; ++j) y[j] += d[j];
             y[6] = du0;
             y[7] = du1;
-            mk = (mk << 1) | UP1;
-            wv.up8_keep(x, y, mk);
+            wv.up8(x, y);
+        }
+        if constexpr (SPLIT) {
+            // the upper half-wave's step statistics take variables 4, 5 and the control step
+            x[4] = wv.lo_half(x[4]);
+            x[5] = wv.lo_half(x[5]);
+            du0 = wv.lo_half(du0);
+            du1 = wv.lo_half(du1);
         }
         const T* xk = x;
         const T duk[2] = {du0, du1};
@@ -1165,13 +1158,16 @@ struct WideSolver {
         // Multipliers of the dynamics rows into stage k from stationarity in s_k:
         //   lam_k = Q_k ds_k + q_k + A_k^T lam_{k+1},   yh+_k = -lam_k
         // (rows 0..5 of the Riccati costate P_k ds_k + p_k), a backward systolic pass:
-        // lane k holds stage k's Hessian diagonal and curvature, gradient and A_k.
+        // lane k holds stage k's Hessian diagonal and curvature, gradient and A_k.  As in
+        // the step recursion no lane is masked: lane 63 keeps its input, and every lane
+        // k >= N (both of the upper half-wave's lanes when SPLIT) holds zero records, so
+        // they hold and pass on zeros and lane N - 1 sees the terminal lam_N = 0.
         wv.mark(3);
-        T lam[6], base[6], ak[8], tva = 0;
+        T lam[6], base[6] = {0, 0, 0, 0, 0, 0}, ak[8], tva = 0;
         {
-            T qd[8], qv[8], cv[6], hvd = 0;
-            if (ks < N) {
-                const int sb = L.ST(ks);
+            if (t < N) {
+                T qd[8], qv[8], cv[6], hvd = 0;
+                const int sb = L.ST(t);
                 ldv<8>(sb + WideLayout::SQD, qd);
                 ldv<8>(sb + WideLayout::SQV, qv);
                 ldv<6>(sb + WideLayout::SCV, cv);  // cv[0..4] = Q00 Q22 Q32 Q55 Q53
@@ -1180,34 +1176,29 @@ struct WideSolver {
                     tva = ld(sb + WideLayout::STV);
                     hvd = ld(sb + WideLayout::SHVD);
                 }
+                const T* x = xk;
+                base[0] = (qd[0] + cv[0]) * x[0] + qv[0];
+                base[1] = qd[1] * x[1] + qv[1];
+                base[2] = (qd[2] + cv[1]) * x[2] + cv[2] * x[3] + qv[2];
+                base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
+                base[4] = qd[4] * x[4] + qv[4];
+                base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
+                if constexpr (MODEL == 1) base[3] += hvd * duk[0];  // (v, w) curvature times the w step
             } else {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) { qd[q] = 0; qv[q] = 0; ak[q] = 0; }
-#pragma unroll
-                for (int q = 0; q < 6; ++q) cv[q] = 0;
+                for (int q = 0; q < 8; ++q) ak[q] = 0;
             }
-            const T* x = xk;
-            base[0] = (qd[0] + cv[0]) * x[0] + qv[0];
-            base[1] = qd[1] * x[1] + qv[1];
-            base[2] = (qd[2] + cv[1]) * x[2] + cv[2] * x[3] + qv[2];
-            base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
-            base[4] = qd[4] * x[4] + qv[4];
-            base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
-            if constexpr (MODEL == 1) base[3] += hvd * duk[0];  // (v, w) curvature times the w step
         }
 #pragma unroll
         for (int q = 0; q < 6; ++q) lam[q] = 0;
-        // (as the step recursion: lane k keeps its multiplier input from step k on, so the
-        // last step's output in lane k is stage k's)
+        // (the last step's output in lane k is stage k's)
         T o[6];
-        unsigned long long md = keep_dn(N);
         for (int s = N - 1; s >= 0; --s) {
             AT_mul(ak, lam, o);
             if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
 #pragma unroll
             for (int q = 0; q < 6; ++q) o[q] += base[q];
-            md = ((md >> 1) & DNM) | DNT;
-            wv.dn6_keep(lam, o, md);
+            wv.dn6(lam, o);
         }
         if (t < N) {
 #pragma unroll

@@ -69,18 +69,20 @@ struct HostWave {
         return r;
     }
     double dn1(double v) const { return from(v, t < 63 ? t + 1 : t); }
-    void up8_keep(double* x, const double* y, unsigned long long keep) const {
+    // device: DPP wave_shr:1 / wave_shl:1 with bound_ctrl off (lane 0 / 63 keeps x)
+    void up8(double* x, const double* y) const {
         for (int q = 0; q < 8; ++q) {
-            const double r = up1(y[q]);
-            if (!((keep >> t) & 1)) x[q] = r;
+            const double r = from(y[q], t > 0 ? t - 1 : t);
+            if (t > 0) x[q] = r;
         }
     }
-    void dn6_keep(double* x, const double* y, unsigned long long keep) const {
+    void dn6(double* x, const double* y) const {
         for (int q = 0; q < 6; ++q) {
-            const double r = dn1(y[q]);
-            if (!((keep >> t) & 1)) x[q] = r;
+            const double r = from(y[q], t < 63 ? t + 1 : t);
+            if (t < 63) x[q] = r;
         }
     }
+    double lo_half(double v) const { return from(v, t & 31); }
     // device: v_permlane32_swap gives the lower half (own, partner), the upper (partner, own)
     void xor32_pair(double v, double& a, double& b) const {
         const double o = from(v, t ^ 32);
