@@ -1,7 +1,12 @@
 """Benchmark: NMPC solves/s of the MPC::Solve hot path on MI355X.
 
     python bench.py [--gpus N --steps K --warmup W --batch B --horizon N]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (multi-GPU)
+
+With --gpus N > 1 and no torch.distributed environment (RANK/WORLD_SIZE unset), the
+process launches N ranks itself -- `python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 ... bench.py <same args>` as a child -- before anything touches
+the GPU, and exits with the child's code.  Under an outside launcher WORLD_SIZE must
+equal --gpus (a mismatch is an error, never a silently smaller run).
 
 A step = one pass of the hot path over one batch: every rank solves its shard of
 B problems (BASELINE.json configs[3]: 524288 problems over 8 GPUs = 65536 per GPU,
@@ -55,6 +60,9 @@ def parse():
     ap.add_argument("--model", default="diffdrive", choices=["diffdrive", "bicycle"],
                     help="dynamics: FG_eval's differential drive, or the kinematic bicycle (BASELINE configs[4]: "
                          "run with --horizon 25)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="launch/shard/gather plumbing only: gloo on CPU, a stub solver that writes each "
+                         "problem's global index (tests/test_bench_launch.py); no GPU, no timing claim")
     ap.add_argument("--mode", default="solve", choices=["solve", "track"],
                     help="solve: MPC::Solve on preprocessed inputs (the metric); track: the whole control "
                          "tick from raw poses and waypoint plans (findBestPath + solve + post-processing)")
@@ -125,8 +133,83 @@ def pmc_profile(name):
         return json.load(f)
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks (one process per GPU) under torch.distributed.run and wait for them.
+    Runs in a parent that has not imported torch: the GPU is touched only by the children."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_main(a):
+    """--selftest: the multi-rank plumbing of main() (shard, gather to rank 0, barrier,
+    max over ranks) on gloo/CPU with a stub solver; rank 0 checks the gathered order."""
+    import torch
+    import torch.distributed as dist
+
+    from mpc_ros_amd import dist as D
+
+    rank, world, _ = D.env_rank_world()
+    if world > 1:
+        dist.init_process_group("gloo")
+    total = a.batch * world
+    start, count = D.shard(total, rank, world)
+    u0 = torch.empty((count, 2), dtype=torch.float64)
+    status = torch.empty(count, dtype=torch.int32)
+
+    def step():
+        idx = torch.arange(start, start + count, dtype=torch.float64)
+        u0[:, 0] = idx
+        u0[:, 1] = -idx
+        status.fill_(1)
+        if world > 1:
+            return D.gather_rows(u0, total), D.gather_rows(status, total)
+        return u0, status
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g_u0, g_st = step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        ok = bool(torch.equal(g_u0[:, 0], torch.arange(total, dtype=torch.float64))) and bool((g_st == 1).all())
+        print(json.dumps({"selftest": True, "n_gpus": world, "steps": a.steps, "total_batch": total,
+                          "gather_ok": ok, "ms_per_step": elapsed / a.steps * 1e3}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world_env}: launch with matching counts")
+    if a.selftest:
+        return selftest_main(a)
     import torch
     import torch.distributed as dist
 
