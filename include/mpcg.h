@@ -13,13 +13,18 @@
  * negative = API / HIP error (message in mpcg_last_error()).  Per-problem solver
  * outcomes are reported in `status` with CppAD::ipopt::solve_result::status_type
  * numbering (mpc_ros/include/cppad/ipopt/solve_result.hpp:30-46): 1 success,
- * 2 maxiter_exceeded, 9 restoration_failure, 10 error_in_step_computation,
- * 11 invalid_number_detected.  As in the reference (mpc_planner.cpp:378, the
- * status is computed and then ignored), the last iterate is always returned.
+ * 2 maxiter_exceeded, 3 stop_at_tiny_step, 4 stop_at_acceptable_point,
+ * 9 restoration_failure, 10 error_in_step_computation, 11 invalid_number_detected,
+ * 14 unknown (Ipopt's CPUTIME_EXCEEDED, solve_callback.hpp:1165-1167: the max_cpu_time
+ * budget below).  As in the reference (mpc_planner.cpp:378, the status is computed and
+ * then ignored), the last iterate is always returned.
  *
  * Threading: one handle per thread; mpcg_set_params must not run concurrently with
  * a solve on the same handle (the reference has an unsynchronised writer here,
- * SURVEY.md §3.3 -- this API makes the ordering the caller's explicit job).
+ * SURVEY.md §3.3 -- this API makes the ordering the caller's explicit job).  A handle's
+ * device scratch (solve order, spill areas, staging) is used stream-ordered: a solve on a
+ * different stream than the handle's previous one first waits for that previous work
+ * (an event), so one thread may queue solves on several streams.
  *
  * Integration (cgo/ctypes/C++ stubs): INTEGRATION.md.
  */
@@ -33,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MPCG_ABI_VERSION 1
+#define MPCG_ABI_VERSION 2
 
 /* The 15 keys of the reference's parameter map (DrivingStateContext::updateMpcConfigs,
  * mpc_ros/src/driving_state.cpp:65-79; MPC::LoadParams mpc_planner.cpp:243-262;
@@ -61,15 +66,43 @@ typedef struct mpcg_params {
     /* Ipopt 3.12 defaults unless changed */
     double tol;               /* 1e-8 */
     int32_t max_iter;         /* 3000 */
-    int32_t filter_cap;       /* filter entries kept per problem (64) */
+    int32_t filter_cap;       /* non-dominated filter entries kept per problem (64; the oldest is
+                                 dropped beyond -- Ipopt's filter is unbounded) */
     double bound_relax_factor;/* 1e-8 */
     double mu_init;           /* 0.1 */
     double wheelbase;         /* model 1 only: Lf [m] */
+    /* "max_cpu_time" (the reference sets 0.5 s, mpc_planner.cpp:368): applied as the number of
+     * iterations the reference's Solve affords in that time at this horizon (CppAD taping and
+     * per-iteration derivative cost measured in the survey: 1.52 ms + 0.225 ms/iteration at
+     * N = 20), so that results are deterministic; beyond it the status is 14 (unknown) with the
+     * last iterate.  >= 1e6: no budget (Ipopt's "no limit"). */
+    double max_cpu_time;
+    /* Ipopt 3.12 defaults (the reference leaves them untouched) */
+    double acceptable_tol;             /* 1e-6 */
+    double acceptable_dual_inf_tol;    /* 1e10 */
+    double acceptable_constr_viol_tol; /* 1e-2 */
+    double acceptable_compl_inf_tol;   /* 1e-2 */
+    double acceptable_obj_change_tol;  /* 1e20 */
+    double kappa_soc;                  /* 0.99 */
+    double soft_resto_pderror_reduction_factor; /* 0.9999 (0: no soft restoration) */
+    double obj_max_inc;                /* 5 */
+    double tiny_step_tol;              /* 10 eps */
+    double tiny_step_y_tol;            /* 1e-2 */
+    int32_t acceptable_iter;           /* 15 (0: no acceptable termination) */
+    int32_t max_soc;                   /* 4 (0: no second-order corrections) */
+    int32_t watchdog_shortened_iter_trigger; /* 10 (0: no watchdog) */
+    int32_t watchdog_trial_iter_max;   /* 3 */
+    int32_t max_soft_resto_iters;      /* 10 */
+    int32_t max_filter_resets;         /* 5 */
+    int32_t filter_reset_trigger;      /* 5 */
+    int32_t reserved;
 } mpcg_params;
 
 typedef struct mpcg_handle mpcg_handle;
 
 int mpcg_abi_version(void);
+/* Hash of the sources the library was built from (mpc_ros_amd/build.py source_hash()). */
+const char* mpcg_build_id(void);
 const char* mpcg_last_error(void);
 
 /* Defaults of an MPC object before LoadParams: MPC::MPC() (mpc_planner.cpp:223-241)
@@ -89,7 +122,8 @@ int mpcg_create(int device, mpcg_handle** out);
 void mpcg_destroy(mpcg_handle* h);
 int mpcg_set_params(mpcg_handle* h, const mpcg_params* p);
 int mpcg_get_params(const mpcg_handle* h, mpcg_params* p);
-/* Device workspace for B problems (bytes); reserve it ahead of graph capture. */
+/* Device workspace for B problems (bytes): the spill areas of the rare solver paths and the
+ * solve-order buffers; reserve it ahead of graph capture. */
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B);
 int mpcg_reserve(mpcg_handle* h, int64_t B);
 
@@ -103,12 +137,10 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
                double* traj, int32_t* status, double* obj, int32_t* iters);
 
 /* Batched solve on device-resident buffers (same layouts), queued on `stream` (a
- * hipStream_t; NULL = the null stream, as everywhere in HIP).  The interior-point
- * iterations are launched in chunks; the call returns once a device-side counter
- * shows every problem terminated (one small event wait per chunk, overlapped with the
- * next chunk).  The outputs are written by the last kernel queued on `stream`:
- * synchronise the stream before reading them on the host.  No allocation if
- * mpcg_reserve(h, B) was called. */
+ * hipStream_t; NULL = the null stream, as everywhere in HIP) without any host
+ * synchronisation: the whole solve is one kernel (plus the solve-order sort for
+ * B > 2048).  Synchronise the stream before reading the outputs on the host.  No
+ * allocation if mpcg_reserve(h, B) was called. */
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
 
@@ -135,11 +167,9 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
                       const double* d_plan, int32_t delay_mode, double* d_cmd, double* d_traj, int32_t* d_status,
                       void* stream);
 
-/* Kernel strategy of the handle's solves (performance only: every strategy runs the
- * same algorithm, results agree to rounding):
- *   MPCG_STRATEGY_AUTO  one problem per wavefront when it fits (steps <= 64), else per lane
- *   MPCG_STRATEGY_LANE  one problem per lane, 64 problems per wavefront, state in HBM
- *   MPCG_STRATEGY_WAVE  one problem per wavefront, the whole problem state in LDS */
+/* Kernel strategy of the handle's solves.  Since ABI 2 there is one: one problem per
+ * wavefront, the whole problem state in LDS (AUTO and WAVE select it).  LANE (the round-1
+ * one-problem-per-lane kernels) was removed; selecting it is an error. */
 #define MPCG_STRATEGY_AUTO 0
 #define MPCG_STRATEGY_LANE 1
 #define MPCG_STRATEGY_WAVE 2

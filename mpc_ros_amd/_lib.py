@@ -28,6 +28,15 @@ class MpcgParams(C.Structure):
         ("max_angvel", C.c_double), ("max_throttle", C.c_double), ("bound", C.c_double),
         ("tol", C.c_double), ("max_iter", C.c_int32), ("filter_cap", C.c_int32),
         ("bound_relax_factor", C.c_double), ("mu_init", C.c_double), ("wheelbase", C.c_double),
+        ("max_cpu_time", C.c_double),
+        ("acceptable_tol", C.c_double), ("acceptable_dual_inf_tol", C.c_double),
+        ("acceptable_constr_viol_tol", C.c_double), ("acceptable_compl_inf_tol", C.c_double),
+        ("acceptable_obj_change_tol", C.c_double), ("kappa_soc", C.c_double),
+        ("soft_resto_pderror_reduction_factor", C.c_double), ("obj_max_inc", C.c_double),
+        ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
+        ("acceptable_iter", C.c_int32), ("max_soc", C.c_int32), ("watchdog_shortened_iter_trigger", C.c_int32),
+        ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32),
+        ("max_filter_resets", C.c_int32), ("filter_reset_trigger", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -37,6 +46,7 @@ _ip = C.POINTER(C.c_int32)
 _PP = C.POINTER(MpcgParams)
 SIGNATURES = {
     "mpcg_abi_version": ([], C.c_int),
+    "mpcg_build_id": ([], C.c_char_p),
     "mpcg_last_error": ([], C.c_char_p),
     "mpcg_params_default": ([_PP], C.c_int),
     "mpcg_params_plugin_default": ([_PP], C.c_int),
@@ -60,7 +70,8 @@ SIGNATURES = {
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
 }
 
-STRATEGY = {"auto": 0, "lane": 1, "wave": 2}
+STRATEGY = {"auto": 0, "lane": 1, "wave": 2}  # (LANE was removed in ABI 2: selecting it raises)
+ABI_VERSION = 2
 
 _lib = None
 
@@ -81,8 +92,14 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.mpcg_abi_version() != 1:
+        if L.mpcg_abi_version() != ABI_VERSION:
             raise MpcgError("libmpcg ABI version mismatch")
+        from . import build
+
+        want, got = build.source_hash(), L.mpcg_build_id().decode()
+        if got != want:
+            raise MpcgError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                            "rebuild with `python -m mpc_ros_amd.build`")
         _lib = L
     return _lib
 

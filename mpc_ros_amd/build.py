@@ -12,10 +12,23 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmpcg.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_kernels.hip", "mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpc_planner.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpc_planner.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h")] + [
     os.path.join(ROOT, "include", f) for f in ("mpcg.h", "mpc_planner.h")]
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
+
+
+def source_hash() -> str:
+    """Hash of every source and header the library is built from (baked into the library
+    as mpcg_build_id(); the loader refuses a library built from other sources)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def hipcc() -> str:
@@ -25,11 +38,18 @@ def hipcc() -> str:
     return "hipcc"
 
 
+def built_id(lib: str = LIB) -> str | None:
+    """mpcg_build_id() of a built library, read from its file (no GPU runtime needed)."""
+    if not os.path.exists(lib):
+        return None
+    with open(lib, "rb") as fh:
+        data = fh.read()
+    i = data.find(b"MPCG-BUILD-ID:")
+    return data[i + 14:i + 30].decode() if i >= 0 else None
+
+
 def stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
+    return built_id() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -37,7 +57,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value",
-           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"']
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
     cmd += SOURCES + ["-o", LIB + ".tmp"]

@@ -29,24 +29,37 @@ struct mpcg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     mpcg_params params{};
-    double* ws = nullptr;
-    size_t ws_bytes = 0;
     // staging buffers for mpcg_solve (host pointers)
     double* d_io = nullptr;
     size_t io_bytes = 0;
-    mpcg::DriverCtx drv;  // device active counter, pinned readback slots, events
     int strategy = MPCG_STRATEGY_AUTO;
     // mpcg_track_device intermediates: state [B][6] | coeffs [B][4] | u0 [B][2]
     double* d_trk = nullptr;
     size_t trk_bytes = 0;
-    // solve-order buffers of the wave strategy (keys, indices, sort scratch)
+    // solve-order buffers (keys, indices, sort scratch)
     void* d_sched = nullptr;
     size_t sched_bytes = 0;
+    // per-problem HBM spill areas of the solver's rare paths
+    double* d_spill = nullptr;
+    size_t spill_bytes = 0;
+    // stream ordering of the scratch above: the last stream that used it and an event
+    // recorded after that use
+    hipStream_t last_stream = nullptr;
+    hipEvent_t last_ev = nullptr;
+    bool have_last = false;
 };
+
+#ifndef MPCG_BUILD_ID
+#define MPCG_BUILD_ID "unversioned"
+#endif
 
 extern "C" {
 
 int mpcg_abi_version(void) { return MPCG_ABI_VERSION; }
+const char* mpcg_build_id(void) {
+    static const char kId[] = MPCG_BUILD_ID;  // "MPCG-BUILD-ID:<source hash>" (mpc_ros_amd/build.py)
+    return std::strncmp(kId, "MPCG-BUILD-ID:", 14) == 0 ? kId + 14 : kId;
+}
 const char* mpcg_last_error(void) { return g_err.c_str(); }
 
 static void ipopt_defaults(mpcg_params* p) {
@@ -57,6 +70,36 @@ static void ipopt_defaults(mpcg_params* p) {
     p->mu_init = 0.1;
     p->wheelbase = 0.5;
     p->model = 0;
+    p->max_cpu_time = 0.5;  // mpc_planner.cpp:368
+    p->acceptable_tol = 1e-6;
+    p->acceptable_dual_inf_tol = 1e10;
+    p->acceptable_constr_viol_tol = 1e-2;
+    p->acceptable_compl_inf_tol = 1e-2;
+    p->acceptable_obj_change_tol = 1e20;
+    p->kappa_soc = 0.99;
+    p->soft_resto_pderror_reduction_factor = 0.9999;
+    p->obj_max_inc = 5.0;
+    p->tiny_step_tol = 10.0 * 2.220446049250313e-16;
+    p->tiny_step_y_tol = 1e-2;
+    p->acceptable_iter = 15;
+    p->max_soc = 4;
+    p->watchdog_shortened_iter_trigger = 10;
+    p->watchdog_trial_iter_max = 3;
+    p->max_soft_resto_iters = 10;
+    p->max_filter_resets = 5;
+    p->filter_reset_trigger = 5;
+}
+
+// max_cpu_time as the iterations the reference's Solve affords in that time at horizon
+// N: CppAD taping 1.52 ms (N = 20) / 3.93 ms (N = 40) and derivative cost 0.225 / 0.467 ms
+// per iteration, measured in the survey, linear in N.  -1: no budget.
+// (oracle/ipm.c ora_cpu_iter_budget restates the same model for the checker.)
+static int cpu_iter_budget(double max_cpu_time, int steps) {
+    if (!(max_cpu_time > 0) || max_cpu_time >= 999999.0) return -1;
+    const double setup = std::fmax(0.0, 0.1205e-3 * steps - 0.89e-3);
+    const double per = std::fmax(0.0121e-3 * steps - 0.017e-3, 1e-5);
+    const double b = std::floor((max_cpu_time - setup) / per);
+    return b < 0 ? 0 : (b > 1e9 ? 1000000000 : (int)b);
 }
 
 int mpcg_params_default(mpcg_params* p) {
@@ -134,6 +177,13 @@ int mpcg_params_set(mpcg_params* p, const char* key, double v) {
 int mpcg_params_check(const mpcg_params* p) {
     if (!p) return fail(-1, "null params");
     if (p->steps < 2 || p->steps > 4096) return fail(-1, "STEPS must be in [2, 4096]");
+    if (!(p->max_cpu_time > 0)) return fail(-1, "max_cpu_time must be > 0");
+    if (p->acceptable_iter < 0 || p->max_soc < 0 || p->watchdog_shortened_iter_trigger < 0 ||
+        p->watchdog_trial_iter_max < 0 || p->max_soft_resto_iters < 0 || p->max_filter_resets < 0 ||
+        p->filter_reset_trigger < 1)
+        return fail(-1, "invalid Ipopt integer option");
+    if (!(p->soft_resto_pderror_reduction_factor >= 0) || !(p->tiny_step_tol >= 0) || !(p->kappa_soc > 0))
+        return fail(-1, "invalid Ipopt option");
     if (!(p->dt > 0) || !std::isfinite(p->dt)) return fail(-1, "DT must be > 0");
     if (!(p->max_angvel > 0) || !(p->max_throttle > 0) || !(p->bound > 0)) return fail(-1, "bounds must be > 0");
     const double w[] = {p->w_cte, p->w_etheta, p->w_v, p->w_angvel, p->w_accel, p->w_angvel_d, p->w_accel_d};
@@ -172,14 +222,34 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
     q.filter_cap = p.filter_cap;
     q.model = p.model;
     q.lf = p.wheelbase;
+    q.acceptable_tol = p.acceptable_tol;
+    q.acceptable_iter = p.acceptable_iter;
+    q.acceptable_dual_inf_tol = p.acceptable_dual_inf_tol;
+    q.acceptable_constr_viol_tol = p.acceptable_constr_viol_tol;
+    q.acceptable_compl_inf_tol = p.acceptable_compl_inf_tol;
+    q.acceptable_obj_change_tol = p.acceptable_obj_change_tol;
+    q.max_soc = p.max_soc;
+    q.kappa_soc = p.kappa_soc;
+    q.watchdog_trigger = p.watchdog_shortened_iter_trigger;
+    q.watchdog_trial_max = p.watchdog_trial_iter_max;
+    q.soft_resto_factor = p.soft_resto_pderror_reduction_factor;
+    q.max_soft_resto_iters = p.max_soft_resto_iters;
+    q.obj_max_inc = p.obj_max_inc;
+    q.max_filter_resets = p.max_filter_resets;
+    q.filter_reset_trigger = p.filter_reset_trigger;
+    q.tiny_step_tol = p.tiny_step_tol;
+    q.tiny_step_y_tol = p.tiny_step_y_tol;
+    q.cpu_iter_budget = cpu_iter_budget(p.max_cpu_time, p.steps);
     return q;
 }
 
+// solve-order buffers (batches beyond the resident wavefronts)
+static const int64_t kOrderMinBatch = 2048;
+
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B) {
     if (!p || B <= 0) return 0;
-    const mpcg::IpmLayout L{p->steps};
-    const size_t tiles = (size_t)((B + 63) / 64);  // one tile of 64 problems per wavefront
-    return (size_t)L.total(p->filter_cap) * sizeof(double) * 64 * tiles;
+    const mpcg::IpmParams P = to_ipm(*p);
+    return mpcg::wide_spill_bytes(P, B) + (B > kOrderMinBatch ? mpcg::wide_sched_bytes(B) : 0);
 }
 
 int mpcg_create(int device, mpcg_handle** out) {
@@ -199,13 +269,10 @@ int mpcg_create(int device, mpcg_handle** out) {
         return hip_fail(e, "hipStreamCreate");
     }
     mpcg_params_plugin_default(&h->params);
-    e = hipMalloc((void**)&h->drv.d_active, sizeof(int));
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h->drv.h_active, 2 * sizeof(int), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drv.ev[0], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drv.ev[1], hipEventDisableTiming);
+    e = hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         mpcg_destroy(h);
-        return hip_fail(e, "driver buffers");
+        return hip_fail(e, "hipEventCreate");
     }
     *out = h;
     return 0;
@@ -215,14 +282,12 @@ void mpcg_destroy(mpcg_handle* h) {
     if (!h) return;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->ws) hipFree(h->ws);
+    if (h->have_last) hipEventSynchronize(h->last_ev);
     if (h->d_io) hipFree(h->d_io);
     if (h->d_trk) hipFree(h->d_trk);
     if (h->d_sched) hipFree(h->d_sched);
-    if (h->drv.d_active) hipFree(h->drv.d_active);
-    if (h->drv.h_active) hipHostFree(h->drv.h_active);
-    for (hipEvent_t ev : h->drv.ev)
-        if (ev) hipEventDestroy(ev);
+    if (h->d_spill) hipFree(h->d_spill);
+    if (h->last_ev) hipEventDestroy(h->last_ev);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -241,24 +306,21 @@ int mpcg_get_params(const mpcg_handle* h, mpcg_params* p) {
     return 0;
 }
 
-static int ensure_ws(mpcg_handle* h, int64_t B) {
-    const size_t need = mpcg_workspace_bytes(&h->params, B);
-    if (need <= h->ws_bytes) return 0;
+static int ensure_spill(mpcg_handle* h, int64_t B) {
+    const size_t need = mpcg::wide_spill_bytes(to_ipm(h->params), B);
+    if (need <= h->spill_bytes) return 0;
     hipSetDevice(h->device);
-    if (h->ws) {
-        hipDeviceSynchronize();  // the old workspace may be in use on any stream
-        hipFree(h->ws);
-        h->ws = nullptr;
-        h->ws_bytes = 0;
+    if (h->d_spill) {
+        hipDeviceSynchronize();  // may be in use on any stream
+        hipFree(h->d_spill);
+        h->d_spill = nullptr;
+        h->spill_bytes = 0;
     }
-    hipError_t e = hipMalloc((void**)&h->ws, need);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-    h->ws_bytes = need;
+    hipError_t e = hipMalloc((void**)&h->d_spill, need);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(spill areas)");
+    h->spill_bytes = need;
     return 0;
 }
-
-// solve-order buffers of the wave strategy (batches beyond the resident wavefronts)
-static const int64_t kOrderMinBatch = 2048;
 
 static int ensure_sched(mpcg_handle* h, int64_t B) {
     const size_t need = mpcg::wide_sched_bytes(B);
@@ -276,34 +338,49 @@ static int ensure_sched(mpcg_handle* h, int64_t B) {
     return 0;
 }
 
-static int resolve_strategy(const mpcg_handle* h);
+// 160 KiB of LDS per CU; one wavefront's problem must fit with room for a second
+static const size_t kWideLdsMax = 64 * 1024;
+
+// The handle's scratch (solve order, spill areas, track intermediates) is used
+// stream-ordered: work queued on stream s first waits for the scratch's last use on
+// another stream, and an event marks each use.
+static int order_on(mpcg_handle* h, hipStream_t s) {
+    if (h->have_last && h->last_stream != s) {
+        hipError_t e = hipStreamWaitEvent(s, h->last_ev, 0);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    }
+    return 0;
+}
+static int record_on(mpcg_handle* h, hipStream_t s) {
+    hipError_t e = hipEventRecord(h->last_ev, s);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    h->last_stream = s;
+    h->have_last = true;
+    return 0;
+}
+
+static bool wave_fits(const mpcg::IpmParams& P) { return P.N <= 64 && mpcg::wide_lds_bytes(P) <= kWideLdsMax; }
 
 int mpcg_reserve(mpcg_handle* h, int64_t B) {
     if (!h) return fail(-1, "null handle");
     if (B < 0) return fail(-1, "negative batch");
-    if (resolve_strategy(h) == MPCG_STRATEGY_WAVE) return B > kOrderMinBatch ? ensure_sched(h, B) : 0;
-    return ensure_ws(h, B);
-}
-
-// 160 KiB of LDS per CU; one wavefront's problem must fit with room for a second
-static const size_t kWideLdsMax = 64 * 1024;
-
-static int resolve_strategy(const mpcg_handle* h) {
-    if (h->strategy != MPCG_STRATEGY_AUTO) return h->strategy;
-    const mpcg::IpmParams P = to_ipm(h->params);
-    return (P.N <= 64 && mpcg::wide_lds_bytes(P) <= kWideLdsMax) ? MPCG_STRATEGY_WAVE : MPCG_STRATEGY_LANE;
+    if (B == 0) return 0;
+    int rc = ensure_spill(h, B);
+    if (rc) return rc;
+    return B > kOrderMinBatch ? ensure_sched(h, B) : 0;
 }
 
 int mpcg_set_strategy(mpcg_handle* h, int32_t strategy) {
     if (!h) return fail(-1, "null handle");
-    if (strategy < MPCG_STRATEGY_AUTO || strategy > MPCG_STRATEGY_WAVE) return fail(-1, "unknown strategy");
+    if (strategy == MPCG_STRATEGY_LANE) return fail(-1, "strategy LANE was removed in ABI 2 (one solver: WAVE)");
+    if (strategy != MPCG_STRATEGY_AUTO && strategy != MPCG_STRATEGY_WAVE) return fail(-1, "unknown strategy");
     h->strategy = strategy;
     return 0;
 }
 
 int mpcg_get_strategy(const mpcg_handle* h) {
     if (!h) return fail(-1, "null handle");
-    return resolve_strategy(h);
+    return MPCG_STRATEGY_WAVE;
 }
 
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
@@ -318,32 +395,27 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
     const mpcg::IpmParams P = to_ipm(h->params);
-    const int strat = resolve_strategy(h);
-    if (strat == MPCG_STRATEGY_WAVE) {
-        if (P.N > 64 || mpcg::wide_lds_bytes(P) > kWideLdsMax)
-            return fail(-1, "strategy WAVE needs steps <= 64 and the problem state within 64 KiB of LDS");
-        // batches larger than the resident wavefronts (8 per CU) are solved in
-        // expected-longest-first order (launch_wide_order)
-        const int32_t* order = nullptr;
-        if (B > kOrderMinBatch) {
-            rc = ensure_sched(h, B);
-            if (rc) return rc;
-            int32_t* ord = nullptr;
-            e = mpcg::launch_wide_order(B, d_coeffs, h->d_sched, h->sched_bytes, &ord, s);
-            if (e != hipSuccess) return hip_fail(e, "solve-order sort");
-            order = ord;
-        }
-        e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, s);
-        if (e != hipSuccess) return hip_fail(e, "wide solve launch");
-        return 0;
-    }
-    if (P.model != 0) return fail(-1, "the bicycle model runs on strategy WAVE only (steps <= 64)");
-    rc = ensure_ws(h, B);
+    if (!wave_fits(P)) return fail(-1, "STEPS must be <= 64 (the problem state must fit 64 KiB of LDS)");
+    rc = ensure_spill(h, B);
     if (rc) return rc;
-    e = mpcg::launch_ipm_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters,
-                               h->ws, h->drv, s);
-    if (e != hipSuccess) return hip_fail(e, "ipm_solve_kernel launch");
-    return 0;
+    if (B > kOrderMinBatch) {
+        rc = ensure_sched(h, B);
+        if (rc) return rc;
+    }
+    rc = order_on(h, s);
+    if (rc) return rc;
+    // batches larger than the resident wavefronts (8 per CU) are solved in
+    // expected-longest-first order (launch_wide_order)
+    const int32_t* order = nullptr;
+    if (B > kOrderMinBatch) {
+        int32_t* ord = nullptr;
+        e = mpcg::launch_wide_order(B, d_coeffs, h->d_sched, h->sched_bytes, &ord, s);
+        if (e != hipSuccess) return hip_fail(e, "solve-order sort");
+        order = ord;
+    }
+    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, h->d_spill, s);
+    if (e != hipSuccess) return hip_fail(e, "wide solve launch");
+    return record_on(h, s);
 }
 
 int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
@@ -439,13 +511,15 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
     double* st = h->d_trk;
     double* cf = st + 6 * B;
     double* u0 = cf + 4 * B;
-    int rc = mpcg_preprocess_device(h, B, M, d_pose, d_vel, d_plan, delay_mode, st, cf, stream);
+    int rc = order_on(h, (hipStream_t)stream);
+    if (rc) return rc;
+    rc = mpcg_preprocess_device(h, B, M, d_pose, d_vel, d_plan, delay_mode, st, cf, stream);
     if (rc) return rc;
     rc = mpcg_solve_device(h, B, st, cf, u0, d_traj, d_status, nullptr, nullptr, stream);
     if (rc) return rc;
     e = mpcg::launch_post(B, h->params.dt, h->params.ref_v, d_vel, u0, d_cmd, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "post-processing launch");
-    return 0;
+    return record_on(h, (hipStream_t)stream);
 }
 
 int mpcg_synchronize(mpcg_handle* h) {

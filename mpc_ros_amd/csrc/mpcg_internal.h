@@ -9,26 +9,14 @@
 
 namespace mpcg {
 
-// Host-side state of the iteration driver (owned by the handle).
-struct DriverCtx {
-    int* d_active = nullptr;   // device counter of problems still iterating
-    int* h_active = nullptr;   // 2 pinned host slots
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    int chunk = 8;             // iterations launched between two counter reads
-};
-
-// Queue the whole solve on `stream`.  Returns once every problem has terminated
-// (the host polls the device counter once per chunk of iterations); the outputs
-// are written by the last kernel queued on `stream`.
-hipError_t launch_ipm_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
-                            double* traj, int32_t* status, double* obj, int32_t* iters, double* ws,
-                            DriverCtx& ctx, hipStream_t stream);
-
 // One problem per wavefront (mpcg_wide.hip): LDS bytes per problem, launch.
 size_t wide_lds_bytes(const IpmParams& P);
+// HBM spill areas of B problems (watchdog, acceptable point, second-order corrections,
+// soft restoration: rare paths that must not cost LDS)
+size_t wide_spill_bytes(const IpmParams& P, int64_t B);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             hipStream_t stream);
+                             double* spill, hipStream_t stream);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the
 // launch that writes the workgroup -> problem map into `buf` (returned in *order).
 size_t wide_sched_bytes(int64_t B);

@@ -24,6 +24,7 @@ struct WideArgs {
     int32_t* status;
     double* obj;
     int32_t* iters;
+    double* spill;         // per-problem HBM spill areas (WideLayout::spill() doubles each)
 };
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
@@ -41,7 +42,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int j = 0; j < 4; ++j) pr.c[j] = a.coeffs[p * 4 + j];
     DevWave wv;
     wv.t = t;
-    WideSolver<DevWave, MODEL, SPLIT> S(a.P, pr, wv);
+    const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
+    WideSolver<DevWave, MODEL, SPLIT> S(a.P, pr, wv, a.spill + p * (int64_t)Lw.spill());
     S.solve();
     const double o = S.objective_out();
     const int N = a.P.N;
@@ -99,11 +101,15 @@ hipError_t launch_wide_order(int64_t B, const double* coeffs, void* buf, size_t 
 }
 
 size_t wide_lds_bytes(const IpmParams& P) { return (size_t)WideLayout(P.N, P.filter_cap, P.model).total() * sizeof(double); }
+size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
+    return (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * sizeof(double) * (size_t)B;
+}
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             hipStream_t stream) {
+                             double* spill, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
+    if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
     const bool split = P.N <= 32;
     const void* fn = P.model == 1 ? (split ? (const void*)k_solve_wide<1, true> : (const void*)k_solve_wide<1, false>)
@@ -115,7 +121,7 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters};
+    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, spill};
     if (P.model == 1 && split)
         hipLaunchKernelGGL((k_solve_wide<1, true>), dim3((unsigned)B), dim3(64), lds, stream, a);
     else if (P.model == 1)

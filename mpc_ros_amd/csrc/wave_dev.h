@@ -15,6 +15,7 @@
 //   lo_half(v)      v of lane t & 31 (v_permlane32_swap);
 //   xor32_pair(v, a, b)  {a, b} = {v, v of lane t ^ 32} (v_permlane32_swap);
 //   any(b), uni(i), uni_d(x)  wave vote; wave-uniform (scalar) copy of lane 0's value;
+//   ballot_prefix(b, &n)  lanes below with b set (stream compaction of the filter), n = total;
 //   lane()          the lane index, recomputed by a volatile v_mbcnt pair: each solver phase
 //                   derives its per-lane LDS offsets from it, so the compiler cannot hoist
 //                   them out of the iteration loop (they were kept live across every phase
@@ -123,6 +124,12 @@ struct DevWaveBase {
         b = __hiloint2double((int)hi[1], (int)lo[1]);
     }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
+    // number of lanes below this one with b set, and (total) the count over the wavefront
+    __device__ __forceinline__ int ballot_prefix(bool b, int* total) const {
+        const unsigned long long m = __ballot(b);
+        *total = __builtin_amdgcn_readfirstlane(__popcll(m));
+        return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    }
     // the lane index, recomputed (volatile: the compiler cannot hoist it or values derived
     // from it out of the solver's loops)
     __device__ __forceinline__ int lane() const {

@@ -79,7 +79,17 @@ struct WideLayout {
     MPCG_HD int RSC() const { return SCR() + 8 * MS + 64; }  // row scales: ra[6] rb[6] 1.0 (+pad)
     MPCG_HD int ZB() const { return RSC() + 16; }            // 8 zeros (an absent column)
     MPCG_HD int FI() const { return RSC() + 24; }
-    MPCG_HD int total() const { return FI() + 2 * cap; }
+    MPCG_HD int C0() const { return FI() + 2 * cap; }  // -c of the initial-state rows (6) + pad
+    MPCG_HD int total() const { return C0() + 8; }
+    // Per-problem HBM spill area (doubles) of the rare paths: the watchdog's stored iterate
+    // and direction (LDS [W(0), YP(N)) = 52N), the last acceptable iterate (W: 10N), the
+    // Newton direction kept while second-order corrections are tried (DW, YP: 16N), the
+    // iterate kept while a soft-restoration step is evaluated (W, ZL, ZU, Y: 36N).
+    MPCG_HD int SP_WD() const { return 0; }
+    MPCG_HD int SP_ACC() const { return 52 * N; }
+    MPCG_HD int SP_SOC() const { return 62 * N; }
+    MPCG_HD int SP_SOFT() const { return 78 * N; }
+    MPCG_HD int spill() const { return 114 * N; }
 };
 
 // MODEL: 0 differential drive (FG_eval), 1 kinematic bicycle -- a template parameter
@@ -102,8 +112,18 @@ struct WideSolver {
     // statistics of the current iterate
     T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
     // line-search / iteration state
-    T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt;
+    T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt, delta_w_used;
     int iter, nf, status;
+    bool acc_pending;  // a step (acc_alpha, acc_z) waits to be applied by the next statistics sweep
+    // filter line-search acceptor (Ipopt FilterLSAcceptor): reference point, switching-
+    // condition powers (-gd)^s_phi and theta^s_theta of the reference, reset heuristic
+    T ref_theta, ref_phi, ref_gd, ref_pgd, ref_pth;
+    int last_rej_filter, count_filter_rej, n_filter_resets;
+    // watchdog, tiny steps, soft restoration, acceptable points (BacktrackingLineSearch,
+    // OptimalityErrorConvergenceCheck)
+    int in_wd, wd_short, wd_trial_iter, tiny_last, tiny_flag, in_soft, soft_count, acc_counter, have_acc;
+    T wd_alpha_test, wd_theta, wd_phi, wd_gd, wd_amax_z, last_mu, last_obj, curr_obj;
+    double* spill;  // this problem's HBM spill area (WideLayout::spill() doubles)
     // SPLIT: the sine/cosine pair of the last trial point (the lane's heading theta or
     // etheta), which the next statistics sweep reuses when that trial point was
     // accepted (the accepted iterate is bitwise the trial point: both are w + alpha dw)
@@ -115,8 +135,9 @@ struct WideSolver {
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
-    MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_)
-        : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf) {}
+    MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_, double* spill_)
+        : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf),
+          spill(spill_) {}
 
     // ------------------------------------------------------ the model
     // F(s, u): FG_eval's dynamics (Lin::next); for the bicycle the heading rows turn by
@@ -328,21 +349,31 @@ struct WideSolver {
     }
 
     // ------------------------------------------------ accept + statistics
-    MPCG_HD void accept_one(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun) const {
-        const T ksig = (T)1e10, iksig = (T)1e-10;
+    MPCG_HD void accept_one(T w, T dwv, T zl, T zu, T lo, T hi, T alpha, T amax_z, T* wn, T* zln, T* zun,
+                            bool clamp = true) const {
         const T rdl = rcp(w - lo), rdu = rcp(hi - w);
         const T dzl = mu * rdl - zl - zl * rdl * dwv;
         const T dzu = mu * rdu - zu + zu * rdu * dwv;
         *wn = w + alpha * dwv;
-        const T rs2 = rcp(*wn - lo), ru2 = rcp(hi - *wn);
         const T a = zl + amax_z * dzl, b = zu + amax_z * dzu;
+        if (clamp) {
+            clamp_z(*wn, a, b, lo, hi, zln, zun);
+        } else {
+            *zln = a;
+            *zun = b;
+        }
+    }
+    // IpoptAlgorithm::AcceptTrialPoint: bound multipliers within kappa_sigma of mu / s
+    MPCG_HD void clamp_z(T w, T a, T b, T lo, T hi, T* zln, T* zun) const {
+        const T ksig = (T)1e10, iksig = (T)1e-10;
+        const T rs2 = rcp(w - lo), ru2 = rcp(hi - w);
         *zln = tmax(tmin(a, ksig * mu * rs2), mu * rs2 * iksig);
         *zun = tmax(tmin(b, ksig * mu * ru2), mu * ru2 * iksig);
     }
 
     // Accept the step (w, z_L, z_U with the step lengths, y towards y+): element-parallel
     // over the 8N entries of the stage-major arrays, 64 per round.
-    MPCG_HD void accept_all(int t, bool acc, T alpha, T amax_z) {
+    MPCG_HD void accept_all(int t, bool acc, T alpha, T amax_z, bool clamp = true) {
         wv.sync();
         if (acc) {
             // element-parallel: element e = 8k + j of the stage-major arrays, 64 per round
@@ -356,7 +387,7 @@ struct WideSolver {
                 if (!(k == N - 1 && j >= 6)) {
                     T wn, zln, zun;
                     accept_one(ld(L.W(k) + j), ld(L.DW(k) + j), ld(L.ZL(k) + j), ld(L.ZU(k) + j), lo, hi,
-                               alpha, amax_z, &wn, &zln, &zun);
+                               alpha, amax_z, &wn, &zln, &zun, clamp);
                     st(L.W(k) + j, wn);
                     st(L.ZL(k) + j, zln);
                     st(L.ZU(k) + j, zun);
@@ -471,6 +502,7 @@ struct WideSolver {
                     const int j = j0 + q;
                     const T wj = hi ? w[4 + q] : w[q];
                     const T c = k == 0 ? wj - (hi ? pr.init[4 + q] : pr.init[q]) : wj - Fprev[q];
+                    if (k == 0) st(L.C0() + j, -c);  // initial-state rows of the Newton system
                     const T rsc = rowscale(j, k);
                     const T cs = rsc * c;
                     th += fabs(cs);
@@ -618,6 +650,7 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                if (k == 0) st(L.C0() + j, -c);  // initial-state rows of the Newton system
                 const T rsc = rowscale(j, k);
                 const T cs = rsc * c;
                 th += fabs(cs);
@@ -1100,10 +1133,11 @@ struct WideSolver {
         }
         T x[8];
         {
-            T w0[6];
-            ldn<6>(L.W(0), w0);
+            // the initial-state rows' right-hand side (-c_0, or a second-order correction's)
+            T c0[6];
+            ldv<6>(L.C0(), c0);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && ks == 0) ? -(w0[j] - pr.init[j]) : (T)0;
+            for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && ks == 0) ? c0[j] : (T)0;
             x[6] = 0;
             x[7] = 0;
         }
@@ -1404,6 +1438,160 @@ struct WideSolver {
         return !anybad && isfinite((double)*phi);
     }
 
+    // ------------------------------------------------------------ HBM spill area
+    // Copy LDS [lds0, lds0 + n) to / from the problem's spill area at sp0: lane t moves
+    // elements t, t + 64, ... both ways, so a lane reads back only what it wrote.
+    MPCG_HD void spill_out(int sp0, int lds0, int n) {
+        const int t = wv.lane();
+        wv.sync();
+        for (int e = t; e < n; e += 64) spill[sp0 + e] = ld(lds0 + e);
+    }
+    MPCG_HD void spill_in(int sp0, int lds0, int n) {
+        const int t = wv.lane();
+        wv.sync();
+        for (int e = t; e < n; e += 64) st(lds0 + e, (T)spill[sp0 + e]);
+        wv.sync();
+    }
+
+    // ------------------------------------------------------------ the filter
+    // Ipopt's FilterLSAcceptor / Filter (oracle/ipm.c: set_ref .. update_for_next).
+    MPCG_HD static bool compare_le(T lhs, T rhs, T bas) {  // IpUtils Compare_le
+        return lhs - rhs <= (T)(10.0 * 2.220446049250313e-16) * (T)fabs(bas);
+    }
+    // the reference point of a line search; the switching-condition powers once per search
+    MPCG_HD void set_ref(T th, T ph, T gd) {
+        ref_theta = wv.uni_d(th);
+        ref_phi = wv.uni_d(ph);
+        ref_gd = wv.uni_d(gd);
+        ref_pgd = 0;
+        ref_pth = 0;
+        if (wv.uni(gd < 0)) {
+            ref_pgd = wv.uni_d((T)pow((double)-gd, 2.3));
+            ref_pth = wv.uni_d((T)pow((double)th, 1.1));
+        }
+    }
+    MPCG_HD bool is_ftype(T alpha_test) const { return ref_gd < 0 && alpha_test * ref_pgd > ref_pth; }
+    MPCG_HD bool armijo_holds(T alpha_test, T phit) const {
+        return compare_le(phit - ref_phi, (T)1e-8 * alpha_test * ref_gd, ref_phi);
+    }
+    MPCG_HD bool acceptable_to_current_iterate(T phit, T thetat) const {
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8;
+        if (phit > ref_phi) {  // obj_max_inc
+            const T basval = fabs(ref_phi) > (T)10 ? (T)log10((double)fabs(ref_phi)) : (T)1;
+            if ((T)log10((double)(phit - ref_phi)) > (T)P.obj_max_inc * basval) return false;
+        }
+        return compare_le(thetat, ((T)1 - gamma_theta) * ref_theta, ref_theta) ||
+               compare_le(phit - ref_phi, -gamma_phi * ref_theta, ref_phi);
+    }
+    // acceptable to the filter: no entry f with theta >= theta_f and phi >= phi_f (lane f tests entry f)
+    MPCG_HD bool filter_ok(T phit, T thetat) {
+        const int t = wv.lane();
+        const int fi = L.FI();
+        bool hit = false;
+        for (int f0 = 0; f0 < nf; f0 += 64) {
+            const int f = f0 + t;
+            const bool h = f < nf && thetat >= ld(fi + 2 * f) && phit >= ld(fi + 2 * f + 1);
+            hit = hit || wv.any(h);
+        }
+        return !hit;
+    }
+    // Filter::AddEntry: the entries the new one dominates are dropped (acceptance does not
+    // change); beyond filter_cap non-dominated entries the oldest is dropped
+    MPCG_HD void filter_add(T ph, T th) {
+        const int t = wv.lane();
+        const int fi = L.FI(), cap = P.filter_cap;
+        int base = 0;
+        for (int f0 = 0; f0 < nf; f0 += 64) {
+            const int f = f0 + t;
+            T e0 = 0, e1 = 0;
+            wv.sync();
+            if (f < nf) {
+                e0 = ld(fi + 2 * f);
+                e1 = ld(fi + 2 * f + 1);
+            }
+            const bool keep = f < nf && !(ph <= e1 && th <= e0);
+            int cnt;
+            const int dst = base + wv.ballot_prefix(keep, &cnt);
+            wv.sync();
+            if (keep) {
+                st(fi + 2 * dst, e0);
+                st(fi + 2 * dst + 1, e1);
+            }
+            base += cnt;
+        }
+        nf = wv.uni(base);
+        int slot = nf;
+        if (nf == cap) {  // full: drop the oldest entry
+            T e0 = 0, e1 = 0;
+            for (int f0 = 0; f0 < cap; f0 += 64) {
+                const int f = f0 + t + 1;
+                wv.sync();
+                if (f < cap) { e0 = ld(fi + 2 * f); e1 = ld(fi + 2 * f + 1); }
+                wv.sync();
+                if (f < cap) { st(fi + 2 * (f - 1), e0); st(fi + 2 * (f - 1) + 1, e1); }
+            }
+            slot = cap - 1;
+        } else {
+            ++nf;
+        }
+        wv.sync();
+        if (t == 0) {
+            st(fi + 2 * slot, th);
+            st(fi + 2 * slot + 1, ph);
+        }
+        wv.sync();
+    }
+    MPCG_HD void augment_filter() {
+        filter_add(ref_phi - (T)1e-8 * ref_theta, ((T)1 - (T)1e-5) * ref_theta);
+    }
+    // FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (with the filter reset heuristic)
+    MPCG_HD bool check_acceptability(T alpha_test, T phit, T thetat) {
+        if (theta_max < 0) theta_max = wv.uni_d((T)1e4 * tmax((T)1, ref_theta));
+        if (theta_min < 0) theta_min = wv.uni_d((T)1e-4 * tmax((T)1, ref_theta));
+        if (wv.uni(thetat > theta_max)) return false;
+        bool accept;
+        if (alpha_test > 0 && is_ftype(alpha_test) && ref_theta <= theta_min)
+            accept = armijo_holds(alpha_test, phit);
+        else
+            accept = acceptable_to_current_iterate(phit, thetat);
+        if (!wv.uni(accept)) {
+            last_rej_filter = 0;
+            return false;
+        }
+        if (!filter_ok(phit, thetat)) {
+            last_rej_filter = 1;
+            return false;
+        }
+        if (P.max_filter_resets > 0 && n_filter_resets < P.max_filter_resets) {
+            if (last_rej_filter) {
+                if (++count_filter_rej >= P.filter_reset_trigger) {
+                    nf = 0;
+                    count_filter_rej = 0;
+                    ++n_filter_resets;
+                }
+            } else {
+                count_filter_rej = 0;
+            }
+        }
+        return true;
+    }
+    // FilterLSAcceptor::UpdateForNextIteration: augment unless an f-type step with Armijo
+    MPCG_HD void update_for_next(T alpha_test, T phit) {
+        if (wv.uni(!is_ftype(alpha_test) || !armijo_holds(alpha_test, phit))) augment_filter();
+    }
+    // FilterLSAcceptor::CalculateAlphaMin (reference point values)
+    MPCG_HD T alpha_min_of() const {
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8;
+        T a;
+        if (ref_gd < 0) {
+            a = tmin(gamma_theta, gamma_phi * ref_theta / -ref_gd);
+            if (ref_theta <= theta_min) a = tmin(a, ref_pth / ref_pgd);
+        } else {
+            a = gamma_theta;
+        }
+        return (T)0.05 * a;
+    }
+
     // ------------------------------------------------------------ phases
     MPCG_HD void init() {
         setup();
@@ -1430,48 +1618,93 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
         }
-        stats(false, (T)0, (T)0);
-        theta_max = wv.uni_d((T)1e4 * tmax((T)1, theta));
-        theta_min = wv.uni_d((T)1e-4 * tmax((T)1, theta));
+        theta_max = -1;
+        theta_min = -1;
         dw_last = 0;
+        delta_w_used = 0;
         acc_alpha = 0;
         acc_z = 0;
+        acc_pending = false;
         iter = 0;
         nf = 0;
         kkt = 0;
+        ref_theta = ref_phi = ref_gd = ref_pgd = ref_pth = 0;
+        last_rej_filter = count_filter_rej = n_filter_resets = 0;
+        in_wd = wd_short = wd_trial_iter = tiny_last = tiny_flag = in_soft = soft_count = acc_counter = have_acc = 0;
+        wd_alpha_test = wd_theta = wd_phi = wd_gd = wd_amax_z = 0;
+        last_mu = -1;
+        last_obj = 0;
+        curr_obj = (T)-1e50;
+        cur_acceptable = false;
     }
 
+    bool cur_acceptable;
+    // Convergence (OptimalityErrorConvergenceCheck::CheckConvergence) and the monotone
+    // barrier update (MonotoneMuUpdate::UpdateBarrierParameter) at the current iterate.
     MPCG_HD int begin() {
-        stats(iter > 0, acc_alpha, acc_z);
+        stats(acc_pending, acc_alpha, acc_z);
+        acc_pending = false;
         const int nbnd = 2 * (8 * N - 2);
         const int ng = 6 * N;
         const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
         const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
         const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
-        const T dual_uns = dual_inf / sf;
-        kkt = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl0)));
+        // unscaled_curr_dual_infeasibility / _complementarity: objective scaling undone
+        const T dual_uns = dual_inf / sf, compl_uns = compl0 / sf;
+        kkt = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl_uns)));
+        // CurrentIsAcceptable (objective bookkeeping once per iteration)
+        last_obj = curr_obj;
+        curr_obj = wv.uni_d(sf * fval);
+        cur_acceptable = wv.uni(E0 <= (T)P.acceptable_tol && dual_uns <= (T)P.acceptable_dual_inf_tol &&
+                                prim_uns <= (T)P.acceptable_constr_viol_tol &&
+                                compl_uns <= (T)P.acceptable_compl_inf_tol &&
+                                fabs(last_obj - curr_obj) / tmax((T)1, (T)fabs(curr_obj)) <=
+                                    (T)P.acceptable_obj_change_tol);
         int s = 0;
         // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
         // drop a NaN; the sums do not)
-        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval))
+        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval)) {
             s = IPM_INVALID_NUMBER;
-        else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl0 <= (T)1e-4)
+        } else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl_uns <= (T)1e-4) {
             s = IPM_SUCCESS;
-        else if (iter == P.max_iter)
-            s = IPM_MAXITER;
+        } else {
+            if (P.acceptable_iter > 0 && cur_acceptable) {
+                if (++acc_counter >= P.acceptable_iter) s = IPM_ACCEPTABLE;
+            } else {
+                acc_counter = 0;
+            }
+            if (!s && iter >= P.max_iter) s = IPM_MAXITER;
+            if (!s && P.cpu_iter_budget >= 0 && iter > P.cpu_iter_budget) s = IPM_UNKNOWN;
+        }
         s = wv.uni(s);
         if (s) return s;
         const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
-        const T mu_min = (T)(P.tol / 10.0);
-        for (;;) {
-            const T complmu = tmax(pmax - mu, mu - pmin);
-            const T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
-            if (wv.uni(Emu > kappa_eps * mu || mu <= mu_min)) break;
-            const T mnew = tmax(mu_min, tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)));
-            if (wv.uni(mnew >= mu)) break;
-            mu = wv.uni_d(mnew);
+        const T mu_min = (T)(fmin(P.tol, 1e-4) / 11.0);  // min(tol, compl_inf_tol) / (kappa_eps + 1)
+        int tf = tiny_flag;
+        tiny_flag = 0;
+        bool done = false;
+        T complmu = tmax(pmax - mu, mu - pmin);
+        T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+        while (wv.uni((Emu <= kappa_eps * mu || tf) && !done)) {
+            const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
+            const bool changed = mnew != mu;
+            if (!changed && tf) return IPM_TINY_STEP;
+            mu = mnew;
             tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
-            nf = 0;
+            if (!changed) {
+                done = true;
+            } else {
+                complmu = tmax(pmax - mu, mu - pmin);
+                Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+                done = Emu > kappa_eps * mu;
+            }
+            if (done && changed) {  // BacktrackingLineSearch::Reset
+                in_soft = 0;
+                in_wd = 0;
+                wd_short = 0;
+                nf = 0;
+            }
+            tf = 0;
         }
         wv.mark(8);
         return 0;
@@ -1494,86 +1727,377 @@ struct WideSolver {
             ++attempt;
             if (wv.uni(delta_w > (T)1e40)) break;
         }
+        delta_w_used = delta_w;
         return ok ? 0 : IPM_ERROR_IN_STEP;
     }
 
-    MPCG_HD int linesearch(const Fwd& F) {
-        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8, delta_sw = 1, gamma_alpha = (T)0.05;
-        const T s_theta = (T)1.1, s_phi = (T)2.3, eta_phi = (T)1e-8;
-        const T phik = sf * fval - mu * logsum;
-        const T thetak = theta;
-        const T gd = F.gd;
-        const int cap = P.filter_cap;
-        // the switching-condition powers are loop invariants of the trial loop, and are
-        // read only when theta_k <= theta_min (the switching condition and alpha_min's
-        // third term); an inlined pow is ~250 instructions, so they are computed only then
-        T pgd = 0, pth = 0;
-        if (wv.uni(gd < 0 && thetak <= theta_min)) {
-            pgd = wv.uni_d((T)pow((double)-gd, (double)s_phi));
-            pth = wv.uni_d((T)pow((double)thetak, (double)s_theta));
+    // Right-hand side of a second-order correction: d_soc = d(trial) + alpha d_soc, i.e.
+    // c_soc = c(w + alpha dw) + alpha c_soc on the dynamics rows (stage table SD) and the
+    // initial-state rows (C0); the trial point is the last one tried (W + alpha DW).
+    MPCG_HD void soc_rhs(T alpha) {
+        const int t = wv.lane();
+        wv.sync();
+        T dn[6] = {0, 0, 0, 0, 0, 0}, c0[6] = {0, 0, 0, 0, 0, 0};
+        if (t < N) {
+            const int k = t;
+            T w[8], cw[8], cd[8];
+            ldn<8>(L.W(k), cw);
+            ldn<8>(L.DW(k), cd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = cw[j] + alpha * cd[j];
+            if (k < N - 1) {
+                T wn[6], cwn[6], cdn[6];
+                ldn<6>(L.W(k + 1), cwn);
+                ldn<6>(L.DW(k + 1), cdn);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) wn[j] = cwn[j] + alpha * cdn[j];
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                T F[6];
+                next_m(ln, w, w + 6, F);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) dn[j] = F[j] - wn[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) c0[j] = -(w[j] - pr.init[j]);
         }
-        T alpha_min;
-        if (gd < 0 && thetak <= theta_min)
-            alpha_min = gamma_alpha * tmin(gamma_theta, tmin(-gamma_phi * thetak / gd, delta_sw * pth / pgd));
-        else if (gd < 0)
-            alpha_min = gamma_alpha * tmin(gamma_theta, -gamma_phi * thetak / gd);
-        else
-            alpha_min = gamma_alpha * gamma_theta;
-        const bool tiny = F.rel < (T)(10.0 * 2.2e-16);
-        T alpha = F.amax_p;
-        bool accepted = false, ftype = false;
-        const int fi = L.FI();
-        c_ok = 0;
-        for (int ls = 0; ls < 60; ++ls) {
-            if (wv.uni(tiny)) { accepted = true; ftype = true; break; }
-            if (wv.uni(alpha < alpha_min)) break;
+        if (t < N - 1) {
+            const int sb = L.ST(t) + WideLayout::SD;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(sb + j, dn[j] + alpha * ld(sb + j));
+        }
+        if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(L.C0() + j, c0[j] + alpha * ld(L.C0() + j));
+        }
+        wv.sync();
+    }
+
+    // FilterLSAcceptor::TrySecondOrderCorrection: up to max_soc corrected steps from the
+    // same factorisation (the Riccati sweep re-run on the same matrix with the corrected
+    // right-hand side); the Newton direction is kept in the spill area meanwhile.
+    MPCG_HD bool try_soc(T alpha_test, T& alpha, T& amax_z, T theta_trial) {
+        if (P.max_soc <= 0) return false;
+        spill_out(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+        spill_out(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+        int count = 0;
+        bool accept = false;
+        T theta_old = 0, alpha_soc = alpha;
+        while (wv.uni(count < P.max_soc && !accept && (count == 0 || theta_trial <= (T)P.kappa_soc * theta_old))) {
+            theta_old = theta_trial;
+            soc_rhs(alpha_soc);
+            riccati(0, delta_w_used);
+            const Fwd F2 = forward(0);
+            alpha_soc = F2.amax_p;
             T phit, thetat;
-            const bool okt = trial(alpha, &phit, &thetat);
-            if (wv.uni(okt && thetat < theta_max)) {
-                // filter test: lane f checks entry f
-                bool hit = false;
-                for (int f0 = 0; f0 < nf; f0 += 64) {
-                    const int f = f0 + t;
-                    const bool h = f < nf && thetat >= ld(fi + 2 * f) && phit >= ld(fi + 2 * f + 1);
-                    hit = hit || wv.any(h);
+            const bool ok = trial(alpha_soc, &phit, &thetat);
+            accept = ok && check_acceptability(alpha_test, phit, thetat);
+            if (accept) {
+                alpha = alpha_soc;
+                amax_z = F2.amax_z;
+                update_for_next(alpha_test, phit);
+            } else {
+                ++count;
+                theta_trial = thetat;
+            }
+        }
+        if (!accept) {
+            spill_in(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+            spill_in(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+        }
+        return accept;
+    }
+
+    // BacktrackingLineSearch::DoBacktrackingLineSearch on the direction in DW / YP (its
+    // statistics F).  Returns whether a trial point was accepted; alpha, amax_z: the step.
+    MPCG_HD bool backtracking(const Fwd& F, bool skip_first, T& alpha, T& amax_z, int& n_steps, bool& eval_error) {
+        const T alpha_max = F.amax_p;
+        const T alpha_min = in_wd ? alpha_max : alpha_min_of();
+        alpha = alpha_max;
+        amax_z = F.amax_z;
+        T alpha_test = in_wd ? wd_alpha_test : alpha;
+        if (skip_first) alpha *= (T)0.5;
+        n_steps = 0;
+        eval_error = false;
+        bool accept = false;
+        c_ok = 0;
+        // (alpha halves towards alpha_min >= 0; the guard only bounds a zero alpha_min)
+        for (int guard = 0; guard < 1100; ++guard) {
+            if (!wv.uni(alpha > alpha_min || n_steps == 0)) break;
+            T phit, thetat;
+            const bool ok = trial(alpha, &phit, &thetat);
+            if (!in_wd) alpha_test = alpha;
+            if (ok) {
+                accept = check_acceptability(alpha_test, phit, thetat);
+            } else {
+                accept = false;
+                eval_error = true;
+            }
+            if (accept) {
+                update_for_next(alpha_test, phit);
+                break;
+            }
+            if (in_wd) break;
+            if (wv.uni(!eval_error && alpha == alpha_max && theta <= thetat)) {
+                accept = try_soc(alpha_test, alpha, amax_z, thetat);
+                if (accept) break;
+            }
+            alpha *= (T)0.5;
+            ++n_steps;
+        }
+        return accept;
+    }
+
+    MPCG_HD void start_watchdog(const Fwd& F) {
+        in_wd = 1;
+        spill_out(L.SP_WD(), 0, 52 * N);  // W, ZL, ZU, DW, Y, YP
+        wd_trial_iter = 0;
+        wd_alpha_test = F.amax_p;
+        wd_amax_z = F.amax_z;
+        wd_theta = ref_theta;
+        wd_phi = ref_phi;
+        wd_gd = ref_gd;
+    }
+    MPCG_HD void stop_watchdog(Fwd& F) {
+        in_wd = 0;
+        spill_in(L.SP_WD(), 0, 52 * N);
+        set_ref(wd_theta, wd_phi, wd_gd);
+        wd_short = 0;
+        F.amax_p = wd_alpha_test;
+        F.amax_z = wd_amax_z;
+        F.gd = wd_gd;
+        // statistics and stage data of the restored iterate
+        c_ok = 0;
+        stats(false, (T)0, (T)0);
+    }
+
+    // Primal-dual system error (1-norms of the dual infeasibility, the scaled constraint
+    // violation and the mu-complementarity, averaged over their 2(8N-2) + 6N + 8N-2
+    // entries) of the iterate in LDS: the soft restoration phase's measure.
+    MPCG_HD T pd_error() {
+        const int t = wv.lane();
+        wv.sync();
+        T du = 0, pr_ = 0, cm = 0;
+        T Fk[6] = {0, 0, 0, 0, 0, 0};
+        T w[8];
+        const int k = t;
+        const bool act = t < N, last = k == N - 1;
+        if (act) {
+            T zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[7] = {0, 0, 0, 0, 0, 0, 0};
+            T twk = dt, tvk = 0;
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                up[0] = ld(L.W(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7);
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                ln.jac(w, dt, a);
+                next_m(ln, w, w + 6, Fk);
+                turn_d(w, w + 6, &twk, &tvk);
+            }
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            T g[6], at[6] = {0, 0, 0, 0, 0, 0}, gu[2] = {0, 0};
+            grad_state(w, g);
+            if (!last) {
+                AT_mul(a, yn, at);
+                if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
+                grad_ctrl(k, um, w + 6, up, gu);
+            }
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T gj = j < 6 ? sf * g[j] + y[j] - at[j] : sf * gu[j - 6] - (j == 6 ? btw : bta);
+                    du += fabs(gj - zl[j] + zu[j]);
+                    cm += fabs((w[j] - vlo(j)) * zl[j] - mu) + fabs((vhi(j) - w[j]) * zu[j] - mu);
                 }
-                if (!hit) {
-                    const bool sw = (gd < 0) && (alpha * pgd > delta_sw * pth);
-                    if (wv.uni(thetak <= theta_min && sw)) {
-                        if (wv.uni(phit <= phik + eta_phi * alpha * gd)) { accepted = true; ftype = true; break; }
-                    } else if (wv.uni(thetat <= ((T)1 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak)) {
-                        accepted = true;
-                        ftype = false;
-                        break;
+            }
+        }
+        T Fprev[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Fprev[j] = wv.up1(Fk[j]);
+        if (act) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                pr_ += fabs(rowscale(j, k) * c);
+            }
+        }
+        T v[3] = {du, pr_, cm};
+        const int op[3] = {RSUM, RSUM, RSUM};
+        reduce<3, true>(v, op);
+        return wv.uni_d((v[0] + v[1] + v[2]) / (T)((8 * N - 2) + 6 * N + 2 * (8 * N - 2)));
+    }
+    // kappa_sigma correction of every bound multiplier (an immediately accepted step)
+    MPCG_HD void clamp_all() {
+        const int t = wv.lane();
+        wv.sync();
+        const T bl[3] = {sl, wl, al}, bh[3] = {su, wu, au};
+        for (int e = t; e < 8 * N; e += 64) {
+            const int k = e >> 3, j = e & 7;
+            if (k == N - 1 && j >= 6) continue;
+            const T lo = j < 6 ? bl[0] : (j == 6 ? bl[1] : bl[2]);
+            const T hi = j < 6 ? bh[0] : (j == 6 ? bh[1] : bh[2]);
+            T zln, zun;
+            clamp_z(ld(L.W(k) + j), ld(L.ZL(k) + j), ld(L.ZU(k) + j), lo, hi, &zln, &zun);
+            st(L.ZL(k) + j, zln);
+            st(L.ZU(k) + j, zun);
+        }
+        wv.sync();
+    }
+    // BacktrackingLineSearch::TrySoftRestoStep: primal and dual step min(alpha_p, alpha_z),
+    // accepted by the original filter (sat) or by a reduction of the primal-dual error
+    MPCG_HD bool try_soft_resto(const Fwd& F, bool& sat) {
+        sat = false;
+        const T a = wv.uni_d(tmin(F.amax_p, F.amax_z));
+        T phit, thetat;
+        const bool ok = trial(a, &phit, &thetat);
+        if (!wv.uni(ok)) return false;
+        if (check_acceptability((T)0, phit, thetat)) {
+            sat = true;
+            acc_alpha = a;
+            acc_z = a;
+            acc_pending = true;
+            return true;
+        }
+        const T ec = pd_error();
+        spill_out(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);  // W, ZL, ZU
+        spill_out(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        accept_all(wv.lane(), true, a, a, false);
+        c_ok = 0;
+        const T et = pd_error();
+        if (wv.uni(et <= (T)P.soft_resto_factor * ec)) {
+            clamp_all();
+            return true;
+        }
+        spill_in(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);
+        spill_in(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        return false;
+    }
+    // max |dy| of the direction (the tiny-step test's multiplier part)
+    MPCG_HD T dy_max() {
+        const int t = wv.lane();
+        wv.sync();
+        T m = 0;
+        if (t < N) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) - ld(L.Y(t) + j)));
+        }
+        return rmax(m);
+    }
+
+    // BacktrackingLineSearch::FindAcceptableTrialPoint.  Returns 0 with the step to take
+    // pending (acc_*) or applied, or a termination status.
+    MPCG_HD int find_trial_point(Fwd F) {
+        if (mu != last_mu) {
+            in_wd = 0;
+            wd_short = 0;
+            last_mu = mu;
+        }
+        if (P.acceptable_iter > 0 && cur_acceptable) {
+            spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
+            have_acc = 1;
+        }
+        const T phik = wv.uni_d(sf * fval - mu * logsum);
+        if (in_wd)
+            set_ref(wd_theta, wd_phi, wd_gd);
+        else
+            set_ref(theta, phik, F.gd);
+        bool accept = false, soft_or_resto = false;
+        int n_steps = 0;
+        T alpha = 0, amax_z = F.amax_z;
+        bool tiny = false;
+        if (P.tiny_step_tol > 0 && wv.uni(F.rel <= (T)P.tiny_step_tol)) tiny = wv.uni(dy_max() <= (T)P.tiny_step_y_tol);
+        if (in_wd && tiny) {
+            stop_watchdog(F);
+            tiny = false;
+        }
+        if (P.watchdog_trigger > 0 && !in_wd && !tiny && !in_soft && wd_short >= P.watchdog_trigger) start_watchdog(F);
+        if (tiny) {
+            alpha = F.amax_p;
+            amax_z = F.amax_z;
+            c_ok = 0;
+            if (tiny_last) tiny_flag = 1;
+            tiny_last = 1;
+            accept = true;
+        } else {
+            tiny_last = 0;
+            if (in_soft) {
+                if (++soft_count > P.max_soft_resto_iters) {
+                    accept = false;
+                } else {
+                    bool sat;
+                    accept = try_soft_resto(F, sat);
+                    if (accept && sat) {
+                        in_soft = 0;
+                        soft_count = 0;
+                    }
+                }
+                soft_or_resto = accept;
+            } else {
+                bool done = false, skip_first = false;
+                while (!done) {
+                    bool eval_error;
+                    accept = backtracking(F, skip_first, alpha, amax_z, n_steps, eval_error);
+                    if (in_wd) {
+                        if (accept) {
+                            in_wd = 0;
+                            done = true;
+                        } else {
+                            ++wd_trial_iter;
+                            if (eval_error || wd_trial_iter > P.watchdog_trial_max) {
+                                stop_watchdog(F);
+                                skip_first = true;
+                            } else {
+                                done = true;
+                                accept = true;
+                            }
+                        }
+                    } else {
+                        done = true;
                     }
                 }
             }
-            alpha *= (T)0.5;
         }
-        if (!accepted) return IPM_RESTORATION_FAILURE;
-        if (!ftype) {
-            int slot = nf;
-            if (nf == cap) {  // full: drop the oldest entry
-                T e0 = 0, e1 = 0;
-                for (int f0 = 0; f0 < cap; f0 += 64) {
-                    const int f = f0 + t + 1;
-                    wv.sync();
-                    if (f < cap) { e0 = ld(fi + 2 * f); e1 = ld(fi + 2 * f + 1); }
-                    wv.sync();
-                    if (f < cap) { st(fi + 2 * (f - 1), e0); st(fi + 2 * (f - 1) + 1, e1); }
+        if (!accept) {
+            if (!in_soft && P.soft_resto_factor > 0) {
+                augment_filter();  // PrepareRestoPhaseStart
+                bool sat;
+                if (try_soft_resto(F, sat)) {
+                    in_soft = !sat;
+                    accept = true;
+                    soft_or_resto = true;
                 }
-                slot = cap - 1;
-            } else {
-                ++nf;
             }
-            wv.sync();
-            if (t == 0) {
-                st(fi + 2 * slot, ((T)1 - gamma_theta) * thetak);
-                st(fi + 2 * slot + 1, phik - gamma_phi * thetak);
+            if (!accept) {
+                if (!in_soft) augment_filter();
+                // almost feasible: the last acceptable iterate, if any, is the result
+                if (wv.uni(theta <= (T)1e-2 * (T)P.tol) && have_acc) {
+                    spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
+                    return IPM_ACCEPTABLE;
+                }
+                // Ipopt enters its feasibility restoration phase here (oracle/ipm.c
+                // perform_restoration); the device solver stops
+                return IPM_RESTORATION_FAILURE;
             }
         }
-        acc_alpha = wv.uni_d(alpha);
-        acc_z = wv.uni_d(F.amax_z);
+        if (!soft_or_resto) {
+            acc_alpha = wv.uni_d(alpha);
+            acc_z = wv.uni_d(amax_z);
+            acc_pending = true;
+            if (n_steps == 0)
+                wd_short = 0;
+            else
+                ++wd_short;
+        }
         wv.mark(7);
         return 0;
     }
@@ -1586,7 +2110,7 @@ struct WideSolver {
             s = newton();
             if (s) { status = s; break; }
             const Fwd F = forward(0);
-            s = linesearch(F);
+            s = find_trial_point(F);
             if (s) { status = s; break; }
             ++iter;
         }

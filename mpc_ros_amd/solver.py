@@ -13,12 +13,13 @@ import numpy as np
 from . import _lib
 from .params import PLUGIN_DEFAULTS
 
-# Ipopt options the reference leaves at their defaults (mpc_planner.cpp:356-368)
-IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor=1e-8, mu_init=0.1)
+# Ipopt options of the reference's solve (mpc_planner.cpp:356-368: max_cpu_time 0.5, the
+# rest Ipopt 3.12 defaults); any mpcg_params field can be overridden by keyword
+IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor=1e-8, mu_init=0.1, max_cpu_time=0.5)
 
 
 class BatchSolver:
-    def __init__(self, device: int = 0, params: dict | None = None, strategy: str = "auto", **ipopt):
+    def __init__(self, device: int = 0, params: dict | None = None, strategy: str = "wave", **ipopt):
         L = _lib.lib()
         h = C.c_void_p()
         _lib.check(L.mpcg_create(int(device), C.byref(h)), "mpcg_create")
@@ -27,8 +28,8 @@ class BatchSolver:
         self.set_params(params if params is not None else PLUGIN_DEFAULTS, **ipopt)
         self.set_strategy(strategy)
 
-    def set_strategy(self, strategy: str = "auto"):
-        """'auto' | 'lane' (one problem per lane) | 'wave' (one problem per wavefront, LDS-resident)."""
+    def set_strategy(self, strategy: str = "wave"):
+        """'wave' (= 'auto'): one problem per wavefront, LDS-resident (the only kernel strategy)."""
         _lib.check(_lib.lib().mpcg_set_strategy(self._h, _lib.STRATEGY[strategy]), "mpcg_set_strategy")
 
     @property
@@ -53,6 +54,8 @@ class BatchSolver:
         opts = dict(IPOPT_DEFAULTS)
         opts.update(ipopt)
         for k, v in opts.items():
+            if not hasattr(p, k):
+                raise AttributeError(f"mpcg_params has no field {k!r}")
             setattr(p, k, v)
         _lib.check(_lib.lib().mpcg_set_params(self._h, C.byref(p)), "mpcg_set_params")
         self.params = p

@@ -2,28 +2,47 @@
  * oracle/ipm.c -- Ipopt 3.12.8 restated (TEST INFRASTRUCTURE ONLY, see ora.h).
  *
  * The reference hands its NLP to CppAD::ipopt::solve (mpc_ros/include/cppad/ipopt/
- * solve.hpp:419-589) which runs IpoptApplication::OptimizeTNLP with the options of
- * mpc_planner.cpp:356-368 (print_level 0, sparse reverse derivatives, max_cpu_time
- * 0.5) and Ipopt defaults otherwise.  Ipopt is not vendored and not in the image,
- * so this file restates its published algorithm (Waechter & Biegler 2006, "On the
- * implementation of an interior-point filter line-search algorithm for large-scale
- * nonlinear programming", Algorithm A + Algorithm IC), with the Ipopt 3.12 defaults:
+ * solve.hpp:419-589) which runs IpoptApplication::OptimizeTNLP (:586) with the options
+ * of mpc_planner.cpp:356-368 (print_level 0, sparse reverse derivatives, max_cpu_time
+ * 0.5) and Ipopt defaults otherwise.  Ipopt is not vendored (pinned only by
+ * assets/document/ipopt_install/ipopt_x86_install_tutorial.md:9) and not in the image,
+ * so this file restates its published algorithm -- Waechter & Biegler, Math. Prog.
+ * 106(1):25-57, 2006 (Algorithm A, Algorithm IC, the filter line search with second-order
+ * corrections, the feasibility restoration phase of section 3.3) -- and the Ipopt 3.12
+ * sources' handling of it.  The Ipopt file/function each part follows is named at the
+ * part (IpIpoptAlg.cpp, IpOptErrorConvCheck.cpp, IpMonotoneMuUpdate.cpp,
+ * IpPDPerturbationHandler.cpp, IpBacktrackingLineSearch.cpp, IpFilterLSAcceptor.cpp,
+ * IpFilter.cpp, IpRestoMinC_1Nrm.cpp, IpRestoIpoptNLP.cpp, IpRestoConvCheck.cpp,
+ * IpRestoIterateInitializer.cpp).  Defaults (3.12):
  *
- *   mu_init 0.1, kappa_eps 10, kappa_mu 0.2, theta_mu 1.5, tau_min 0.99,
- *   bound_push = bound_frac = 0.01 (and the slack_* equivalents), bound_mult_init 1,
+ *   mu_init 0.1, barrier_tol_factor 10, mu_linear_decrease_factor 0.2,
+ *   mu_superlinear_decrease_power 1.5, mu_min = min(tol, compl_inf_tol)/(kappa_eps + 1),
+ *   tau_min 0.99, bound_push = bound_frac = 0.01, bound_mult_init_val 1,
  *   constr_mult_init_max 1000 (least-squares y0), kappa_sigma 1e10, kappa_d 1e-5,
- *   gamma_theta 1e-5, gamma_phi 1e-8, delta 1, gamma_alpha 0.05, s_theta 1.1,
- *   s_phi 2.3, eta_phi 1e-8, theta_max 1e4*max(1,theta0), theta_min 1e-4*max(1,theta0),
+ *   gamma_theta 1e-5, gamma_phi 1e-8, delta 1, alpha_min_frac 0.05, s_theta 1.1,
+ *   s_phi 2.3, eta_phi 1e-8, theta_max_fact 1e4, theta_min_fact 1e-4, obj_max_inc 5,
+ *   max_soc 4, kappa_soc 0.99, watchdog_shortened_iter_trigger 10,
+ *   watchdog_trial_iter_max 3, soft_resto_pderror_reduction_factor 0.9999,
+ *   max_soft_resto_iters 10, max_filter_resets 5, filter_reset_trigger 5,
+ *   tiny_step_tol 10 eps, tiny_step_y_tol 1e-2,
  *   inertia correction delta_w0 1e-4, delta_w_min 1e-20, delta_w_max 1e40,
  *   kappa_w- 1/3, kappa_w+ 8, kappa_w+bar 100, delta_c 1e-8 mu^0.25,
  *   bound_relax_factor 1e-8 (capped by constr_viol_tol 1e-4), honor_original_bounds,
  *   gradient-based NLP scaling (nlp_scaling_max_gradient 100),
- *   termination: scaled E_0 <= tol (s_max 100) and dual_inf_tol 1,
- *   constr_viol_tol 1e-4, compl_inf_tol 1e-4.
+ *   termination: scaled E_0 <= tol (s_max 100), dual_inf_tol 1, constr_viol_tol 1e-4,
+ *   compl_inf_tol 1e-4; acceptable_tol 1e-6 for acceptable_iter 15 iterations
+ *   (acceptable_dual_inf_tol 1e10, acceptable_constr_viol_tol 1e-2,
+ *   acceptable_compl_inf_tol 1e-2, acceptable_obj_change_tol 1e20);
+ *   restoration phase: resto_penalty_parameter 1000, resto_proximity_weight 1,
+ *   required_infeasibility_reduction 0.9, constr_mult_reset_threshold 0,
+ *   bound_mult_reset_threshold 1000.
  *
- * Not restated (documented in DESIGN.md): second-order corrections, the feasibility
- * restoration phase (a line-search failure returns RESTORATION_FAILURE), the
- * watchdog (off by default in Ipopt), and "acceptable" termination.
+ * Not restated (documented in DESIGN.md): Ipopt's iterative refinement of the KKT
+ * solution (the dense LDL^T solve here is accurate to rounding), slack moves for
+ * slacks below eps*mu (AdjustedTrialSlacks; slacks here stay >= ~1e-11), and a
+ * restoration phase inside the restoration phase (a failed line search of the
+ * restoration problem returns RESTORATION_FAILURE).  The restoration phase is
+ * restated for equality-constrained problems (the MPC NLP has no inequality rows).
  */
 #include <math.h>
 #include <stdio.h>
@@ -32,459 +51,1271 @@
 #include "ora.h"
 
 #define INF_BOUND 1e19
+#define EPS_MACH 2.220446049250313e-16
 
 void ora_ipm_default_opts(ora_ipm_opts* o) {
+    memset(o, 0, sizeof *o);
     o->tol = 1e-8;
     o->max_iter = 3000;
     o->bound_relax_factor = 1e-8;
     o->honor_original_bounds = 1;
     o->mu_init = 0.1;
     o->print_level = 0;
+    o->acceptable_tol = 1e-6;
+    o->acceptable_iter = 15;
+    o->acceptable_dual_inf_tol = 1e10;
+    o->acceptable_constr_viol_tol = 1e-2;
+    o->acceptable_compl_inf_tol = 1e-2;
+    o->acceptable_obj_change_tol = 1e20;
+    o->max_soc = 4;
+    o->kappa_soc = 0.99;
+    o->watchdog_shortened_iter_trigger = 10;
+    o->watchdog_trial_iter_max = 3;
+    o->soft_resto_pderror_reduction_factor = 0.9999;
+    o->max_soft_resto_iters = 10;
+    o->restoration = 1;
+    o->obj_max_inc = 5.0;
+    o->max_filter_resets = 5;
+    o->filter_reset_trigger = 5;
+    o->tiny_step_tol = 10.0 * EPS_MACH;
+    o->tiny_step_y_tol = 1e-2;
+    o->cpu_iter_budget = -1;
 }
 
+int ora_cpu_iter_budget(double max_cpu_time, int steps) {
+    if (!(max_cpu_time > 0) || max_cpu_time >= 999999.0) return -1;  /* Ipopt: no limit at >= 1e6 */
+    const double setup = fmax(0.0, 0.1205e-3 * steps - 0.89e-3);     /* 1.52 ms @20, 3.93 ms @40 */
+    const double per = fmax(0.0121e-3 * steps - 0.017e-3, 1e-5);      /* 0.225 ms @20, 0.467 ms @40 */
+    const double b = floor((max_cpu_time - setup) / per);
+    return b < 0 ? 0 : (b > 1e9 ? 1000000000 : (int)b);
+}
+
+/* ------------------------------------------------------------------ problem */
+/* The problem in Ipopt's internal form: min f(w) s.t. c(w) = 0, wl <= w <= wu, with f and
+ * c already scaled (OrigIpoptNLP + gradient-based scaling, or RestoIpoptNLP on top of it). */
+typedef struct iprob iprob;
+struct iprob {
+    int nw, m;
+    void* ctx;
+    double (*f)(iprob*, const double* w, double mu);
+    void (*grad)(iprob*, const double* w, double mu, double* g);
+    void (*cons)(iprob*, const double* w, double* c);
+    void (*jac)(iprob*, const double* w, double* A);                                    /* m x nw row-major */
+    void (*hess)(iprob*, const double* w, double sigma, double mu, const double* y, double* W); /* nw x nw */
+    double *wl, *wu;
+    char *hasL, *hasU;
+    double obj_scale;  /* for the unscaled termination tests (1 in the restoration problem) */
+    double* c_scale;   /* per row (NULL: 1) */
+};
+
+/* --- the user's NLP with inequality slacks and gradient-based scaling (OrigIpoptNLP) --- */
 typedef struct {
     const ora_nlp* nlp;
-    int n, m, nw, mI;
-    int* ineq_of_row;   /* row -> slack index or -1 */
+    int n, m, mI;
+    int* ineq_of_row;
     double obj_scale;
-    double* c_scale;    /* per constraint row */
-    double *wl, *wu;    /* relaxed bounds on w = (x, s) */
-    char *hasL, *hasU;
-    /* work */
-    double *gf, *gv, *jac, *hess, *lam_unscaled;
-} ipm_ctx;
+    double* c_scale;
+    double *gv, *jac, *lam, *H;
+} orig_ctx;
+
+static double orig_f(iprob* P, const double* w, double mu) {
+    (void)mu;
+    orig_ctx* o = (orig_ctx*)P->ctx;
+    return o->obj_scale * o->nlp->f(o->nlp->ctx, w);
+}
+static void orig_grad(iprob* P, const double* w, double mu, double* g) {
+    (void)mu;
+    orig_ctx* o = (orig_ctx*)P->ctx;
+    o->nlp->grad_f(o->nlp->ctx, w, g);
+    for (int i = 0; i < o->n; ++i) g[i] *= o->obj_scale;
+    for (int i = o->n; i < P->nw; ++i) g[i] = 0.0;
+}
+static void orig_cons(iprob* P, const double* w, double* c) {
+    orig_ctx* o = (orig_ctx*)P->ctx;
+    const ora_nlp* p = o->nlp;
+    p->g(p->ctx, w, o->gv);
+    for (int r = 0; r < o->m; ++r) {
+        int s = o->ineq_of_row[r];
+        double v = (s < 0) ? o->gv[r] - p->gl[r] : o->gv[r] - w[o->n + s];
+        c[r] = o->c_scale[r] * v;
+    }
+}
+static void orig_jac(iprob* P, const double* w, double* A) {
+    orig_ctx* o = (orig_ctx*)P->ctx;
+    const ora_nlp* p = o->nlp;
+    p->jac_g(p->ctx, w, o->jac);
+    for (int r = 0; r < o->m; ++r) {
+        double* row = A + (size_t)r * P->nw;
+        for (int j = 0; j < o->n; ++j) row[j] = o->c_scale[r] * o->jac[(size_t)r * o->n + j];
+        for (int j = o->n; j < P->nw; ++j) row[j] = 0.0;
+        int s = o->ineq_of_row[r];
+        if (s >= 0) row[o->n + s] = -o->c_scale[r];
+    }
+}
+static void orig_hess(iprob* P, const double* w, double sigma, double mu, const double* y, double* W) {
+    (void)mu;
+    orig_ctx* o = (orig_ctx*)P->ctx;
+    const int n = o->n, nw = P->nw;
+    for (int r = 0; r < o->m; ++r) o->lam[r] = y[r] * o->c_scale[r];
+    o->nlp->hess(o->nlp->ctx, w, sigma * o->obj_scale, o->lam, o->H);
+    memset(W, 0, sizeof(double) * (size_t)nw * nw);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) W[(size_t)i * nw + j] = o->H[(size_t)i * n + j];
+}
+
+/* --- the restoration problem (RestoIpoptNLP, equality rows only) ---
+ *   min  rho sum(p + n) + eta(mu)/2 ||D_R (x - x_R)||^2,  eta(mu) = resto_proximity_weight sqrt(mu),
+ *   s.t. c(x) - p + n = 0,  x in the (relaxed) bounds of the original,  p, n >= 0,
+ *   D_R = diag(1 / max(1, |x_R|)); c is the scaled constraint of the original problem. */
+typedef struct {
+    iprob* orig;
+    int nx, m;
+    double rho;
+    const double *xR, *DR;
+    double *c, *A;
+} resto_ctx;
+
+static double resto_f(iprob* P, const double* v, double mu) {
+    resto_ctx* r = (resto_ctx*)P->ctx;
+    const double eta = sqrt(mu);
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < 2 * r->m; ++i) s += v[r->nx + i];
+    for (int i = 0; i < r->nx; ++i) {
+        double d = r->DR[i] * (v[i] - r->xR[i]);
+        q += d * d;
+    }
+    return r->rho * s + 0.5 * eta * q;
+}
+static void resto_grad(iprob* P, const double* v, double mu, double* g) {
+    resto_ctx* r = (resto_ctx*)P->ctx;
+    const double eta = sqrt(mu);
+    for (int i = 0; i < r->nx; ++i) g[i] = eta * r->DR[i] * r->DR[i] * (v[i] - r->xR[i]);
+    for (int i = 0; i < 2 * r->m; ++i) g[r->nx + i] = r->rho;
+}
+static void resto_cons(iprob* P, const double* v, double* c) {
+    resto_ctx* r = (resto_ctx*)P->ctx;
+    r->orig->cons(r->orig, v, c);
+    for (int i = 0; i < r->m; ++i) c[i] += -v[r->nx + i] + v[r->nx + r->m + i];
+}
+static void resto_jac(iprob* P, const double* v, double* A) {
+    resto_ctx* r = (resto_ctx*)P->ctx;
+    const int nv = P->nw;
+    r->orig->jac(r->orig, v, r->A);
+    memset(A, 0, sizeof(double) * (size_t)r->m * nv);
+    for (int i = 0; i < r->m; ++i) {
+        memcpy(A + (size_t)i * nv, r->A + (size_t)i * r->nx, sizeof(double) * r->nx);
+        A[(size_t)i * nv + r->nx + i] = -1.0;
+        A[(size_t)i * nv + r->nx + r->m + i] = 1.0;
+    }
+}
+static void resto_hess(iprob* P, const double* v, double sigma, double mu, const double* y, double* W) {
+    resto_ctx* r = (resto_ctx*)P->ctx;
+    const int nv = P->nw, nx = r->nx;
+    double* Wx = (double*)malloc(sizeof(double) * (size_t)nx * nx);
+    r->orig->hess(r->orig, v, 0.0, mu, y, Wx);  /* constraint curvature only */
+    memset(W, 0, sizeof(double) * (size_t)nv * nv);
+    const double eta = sqrt(mu);
+    for (int i = 0; i < nx; ++i) {
+        for (int j = 0; j < nx; ++j) W[(size_t)i * nv + j] = Wx[(size_t)i * nx + j];
+        W[(size_t)i * nv + i] += sigma * eta * r->DR[i] * r->DR[i];
+    }
+    free(Wx);
+}
+
+/* ------------------------------------------------------------------ solver */
+typedef struct ipm ipm;
+struct ipm {
+    iprob* P;
+    const ora_ipm_opts* o;
+    int nw, m, K, nbnd;
+    int is_resto;
+    ipm* outer;        /* restoration phase: the original problem's solver */
+    int* iter;         /* shared iteration counter (the restoration phase counts on) */
+    /* iterate, direction (the Newton step), actual step (SOC), trial point */
+    double *w, *y, *zL, *zU;
+    double *dw, *dy, *dzL, *dzU;
+    double *aw, *ay, *azL, *azU;
+    double *wt, *yt, *zLt, *zUt;
+    double *gf, *cv, *A, *W, *gphi, *rd, *ct, *csoc, *gft, *At, *rdt;
+    double *KKT, *rhs;
+    int* ipiv;
+    double mu, tau, dw_last;
+    /* statistics of the current iterate */
+    double f, theta, phi, E0, dual_inf, prim_inf, compl0, dual_uns, prim_uns, compl_uns, gd;
+    double sd, sc;
+    /* filter line search acceptor (IpFilterLSAcceptor.cpp) */
+    double *fth, *fph;
+    int nf, capf;
+    double theta_max, theta_min;
+    double ref_theta, ref_phi, ref_gd;
+    int last_rej_filter, count_filter_rej, n_filter_resets;
+    /* watchdog (IpBacktrackingLineSearch.cpp) */
+    int in_wd, wd_short, wd_trial_iter;
+    double wd_alpha_test, wd_theta, wd_phi, wd_gd, last_mu;
+    double *wd_w, *wd_y, *wd_zL, *wd_zU, *wd_dw, *wd_dy, *wd_dzL, *wd_dzU;
+    int tiny_last, tiny_flag;
+    int in_soft, soft_count;
+    /* acceptable-point tracking (IpOptErrorConvCheck.cpp) */
+    int acc_counter, last_obj_iter;
+    double last_obj, curr_obj;
+    int have_acc;
+    double *acc_w, *acc_y, *acc_zL, *acc_zU;
+    int resto_first;   /* restoration problem: first convergence check */
+    ora_ipm_result* diag;
+    double* mem;
+};
 
 static double amax(int n, const double* v) {
     double m = 0.0;
     for (int i = 0; i < n; ++i) m = fmax(m, fabs(v[i]));
     return m;
 }
-
-/* scaled objective */
-static double eval_f(ipm_ctx* c, const double* w) { return c->obj_scale * c->nlp->f(c->nlp->ctx, w); }
-
-static void eval_grad(ipm_ctx* c, const double* w, double* g) {
-    c->nlp->grad_f(c->nlp->ctx, w, g);
-    for (int i = 0; i < c->n; ++i) g[i] *= c->obj_scale;
-    for (int i = c->n; i < c->nw; ++i) g[i] = 0.0;
-}
-
-/* scaled constraint residual c(w): eq rows g - gl; ineq rows g - s */
-static void eval_c(ipm_ctx* c, const double* w, double* cv) {
-    const ora_nlp* p = c->nlp;
-    p->g(p->ctx, w, c->gv);
-    for (int r = 0; r < c->m; ++r) {
-        int s = c->ineq_of_row[r];
-        double v = (s < 0) ? c->gv[r] - p->gl[r] : c->gv[r] - w[c->n + s];
-        cv[r] = c->c_scale[r] * v;
-    }
-}
-
-/* scaled Jacobian of c wrt w, dense m x nw row-major */
-static void eval_A(ipm_ctx* c, const double* w, double* A) {
-    const ora_nlp* p = c->nlp;
-    p->jac_g(p->ctx, w, c->jac);
-    for (int r = 0; r < c->m; ++r) {
-        double* row = A + (size_t)r * c->nw;
-        for (int j = 0; j < c->n; ++j) row[j] = c->c_scale[r] * c->jac[(size_t)r * c->n + j];
-        for (int j = c->n; j < c->nw; ++j) row[j] = 0.0;
-        int s = c->ineq_of_row[r];
-        if (s >= 0) row[c->n + s] = -c->c_scale[r];
-    }
-}
-
-/* scaled Lagrangian Hessian (x block), full n x n */
-static void eval_W(ipm_ctx* c, const double* w, const double* y, double* W) {
-    for (int r = 0; r < c->m; ++r) c->lam_unscaled[r] = y[r] * c->c_scale[r];
-    c->nlp->hess(c->nlp->ctx, w, c->obj_scale, c->lam_unscaled, W);
-}
-
-static double barrier_phi(ipm_ctx* c, const double* w, double mu, int* ok) {
-    const double kd = 1e-5;
-    double phi = eval_f(c, w);
-    *ok = 1;
-    for (int i = 0; i < c->nw; ++i) {
-        if (c->hasL[i]) {
-            double d = w[i] - c->wl[i];
-            if (!(d > 0)) { *ok = 0; return INFINITY; }
-            phi -= mu * log(d);
-            if (!c->hasU[i]) phi += kd * mu * d;
-        }
-        if (c->hasU[i]) {
-            double d = c->wu[i] - w[i];
-            if (!(d > 0)) { *ok = 0; return INFINITY; }
-            phi -= mu * log(d);
-            if (!c->hasL[i]) phi += kd * mu * d;
-        }
-    }
-    if (!isfinite(phi)) *ok = 0;
-    return phi;
-}
-
-static void barrier_grad(ipm_ctx* c, const double* w, double mu, const double* gf, double* gphi) {
-    const double kd = 1e-5;
-    for (int i = 0; i < c->nw; ++i) {
-        double g = gf[i];
-        if (c->hasL[i]) {
-            g -= mu / (w[i] - c->wl[i]);
-            if (!c->hasU[i]) g += kd * mu;
-        }
-        if (c->hasU[i]) {
-            g += mu / (c->wu[i] - w[i]);
-            if (!c->hasL[i]) g -= kd * mu;
-        }
-        gphi[i] = g;
-    }
-}
-
 static double l1(int n, const double* v) {
     double s = 0.0;
     for (int i = 0; i < n; ++i) s += fabs(v[i]);
     return s;
 }
+/* IpUtils.cpp Compare_le: lhs - rhs <= 10 eps |BasVal| */
+static int compare_le(double lhs, double rhs, double bas) { return lhs - rhs <= 10.0 * EPS_MACH * fabs(bas); }
 
-typedef struct { double th, ph; } fpair;
+static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
+    memset(S, 0, sizeof *S);
+    S->P = P;
+    S->o = o;
+    S->nw = P->nw;
+    S->m = P->m;
+    S->K = P->nw + P->m;
+    const size_t nw = P->nw, m = P->m, K = S->K;
+    S->mem = (double*)calloc(40 * nw + 20 * m + 2 * m * nw + nw * nw + K * K + 2 * K + 16, sizeof(double));
+    double* p = S->mem;
+#define TAKE(ptr, cnt) do { S->ptr = p; p += (cnt); } while (0)
+    TAKE(w, nw); TAKE(y, m); TAKE(zL, nw); TAKE(zU, nw);
+    TAKE(dw, nw); TAKE(dy, m); TAKE(dzL, nw); TAKE(dzU, nw);
+    TAKE(aw, nw); TAKE(ay, m); TAKE(azL, nw); TAKE(azU, nw);
+    TAKE(wt, nw); TAKE(yt, m); TAKE(zLt, nw); TAKE(zUt, nw);
+    TAKE(gf, nw); TAKE(cv, m); TAKE(A, m * nw); TAKE(W, nw * nw); TAKE(gphi, nw); TAKE(rd, nw);
+    TAKE(ct, m); TAKE(csoc, m); TAKE(gft, nw); TAKE(At, m * nw); TAKE(rdt, nw);
+    TAKE(KKT, K * K); TAKE(rhs, K);
+    TAKE(wd_w, nw); TAKE(wd_y, m); TAKE(wd_zL, nw); TAKE(wd_zU, nw);
+    TAKE(wd_dw, nw); TAKE(wd_dy, m); TAKE(wd_dzL, nw); TAKE(wd_dzU, nw);
+    TAKE(acc_w, nw); TAKE(acc_y, m); TAKE(acc_zL, nw); TAKE(acc_zU, nw);
+#undef TAKE
+    S->ipiv = (int*)malloc(sizeof(int) * K);
+    S->capf = 64;
+    S->fth = (double*)malloc(sizeof(double) * S->capf);
+    S->fph = (double*)malloc(sizeof(double) * S->capf);
+    for (int i = 0; i < P->nw; ++i) S->nbnd += P->hasL[i] + P->hasU[i];
+    S->theta_max = -1.0;
+    S->theta_min = -1.0;
+    S->last_obj_iter = -1;
+    S->curr_obj = -1e50;
+    S->last_mu = -1.0;
+}
+static void ipm_free(ipm* S) {
+    free(S->mem);
+    free(S->ipiv);
+    free(S->fth);
+    free(S->fph);
+}
 
-int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out, double* zl_out,
-                  double* zu_out, double* lambda_out, double* g_out, ora_ipm_result* res) {
+/* barrier function phi_mu(w) (IpIpoptCalculatedQuantities.cpp curr_barrier_obj), with
+ * the kappa_d damping of one-sided bounds; ok = 0 outside the bounds or not finite */
+static double barrier_phi(ipm* S, const double* w, int* ok) {
+    iprob* P = S->P;
+    const double kd = 1e-5, mu = S->mu;
+    double phi = P->f(P, w, mu);
+    *ok = 1;
+    for (int i = 0; i < S->nw; ++i) {
+        if (P->hasL[i]) {
+            double d = w[i] - P->wl[i];
+            if (!(d > 0)) { *ok = 0; return INFINITY; }
+            phi -= mu * log(d);
+            if (!P->hasU[i]) phi += kd * mu * d;
+        }
+        if (P->hasU[i]) {
+            double d = P->wu[i] - w[i];
+            if (!(d > 0)) { *ok = 0; return INFINITY; }
+            phi -= mu * log(d);
+            if (!P->hasL[i]) phi += kd * mu * d;
+        }
+    }
+    if (!isfinite(phi)) *ok = 0;
+    return phi;
+}
+static void barrier_grad(ipm* S, const double* w, const double* gf, double* gphi) {
+    iprob* P = S->P;
+    const double kd = 1e-5, mu = S->mu;
+    for (int i = 0; i < S->nw; ++i) {
+        double g = gf[i];
+        if (P->hasL[i]) {
+            g -= mu / (w[i] - P->wl[i]);
+            if (!P->hasU[i]) g += kd * mu;
+        }
+        if (P->hasU[i]) {
+            g += mu / (P->wu[i] - w[i]);
+            if (!P->hasL[i]) g -= kd * mu;
+        }
+        gphi[i] = g;
+    }
+}
+
+/* gradient of the Lagrangian rd = gf + A^T y - zL + zU */
+static void lag_grad(ipm* S, const double* gf, const double* A, const double* y, const double* zL, const double* zU,
+                     double* rd) {
+    for (int i = 0; i < S->nw; ++i) rd[i] = gf[i] - zL[i] + zU[i];
+    for (int r = 0; r < S->m; ++r)
+        for (int j = 0; j < S->nw; ++j) rd[j] += A[(size_t)r * S->nw + j] * y[r];
+}
+
+/* complementarity max |s z - mu_t| (NORM_MAX) or sum (NORM_1) */
+static double compl_norm(ipm* S, const double* w, const double* zL, const double* zU, double mu_t, int one) {
+    iprob* P = S->P;
+    double c = 0.0;
+    for (int i = 0; i < S->nw; ++i) {
+        if (P->hasL[i]) {
+            double v = fabs((w[i] - P->wl[i]) * zL[i] - mu_t);
+            c = one ? c + v : fmax(c, v);
+        }
+        if (P->hasU[i]) {
+            double v = fabs((P->wu[i] - w[i]) * zU[i] - mu_t);
+            c = one ? c + v : fmax(c, v);
+        }
+    }
+    return c;
+}
+
+/* evaluate the current iterate: gf, c, A, the optimality-error statistics */
+static void eval_current(ipm* S) {
+    iprob* P = S->P;
+    P->grad(P, S->w, S->mu, S->gf);
+    P->cons(P, S->w, S->cv);
+    P->jac(P, S->w, S->A);
+    S->f = P->f(P, S->w, S->mu);
+    lag_grad(S, S->gf, S->A, S->y, S->zL, S->zU, S->rd);
+    const int m = S->m, nbnd = S->nbnd;
+    /* ComputeOptimalityErrorScaling (s_max 100) */
+    S->sd = fmax(100.0, (l1(m, S->y) + l1(S->nw, S->zL) + l1(S->nw, S->zU)) / (double)(m + nbnd > 0 ? m + nbnd : 1)) / 100.0;
+    S->sc = fmax(100.0, (l1(S->nw, S->zL) + l1(S->nw, S->zU)) / (double)(nbnd > 0 ? nbnd : 1)) / 100.0;
+    S->dual_inf = amax(S->nw, S->rd);
+    S->prim_inf = amax(m, S->cv);
+    S->theta = l1(m, S->cv);
+    S->compl0 = compl_norm(S, S->w, S->zL, S->zU, 0.0, 0);
+    S->E0 = fmax(S->dual_inf / S->sd, fmax(S->prim_inf, S->compl0 / S->sc));
+    /* unscaled_curr_dual_infeasibility / unscaled_curr_nlp_constraint_violation /
+     * unscaled_curr_complementarity: objective scaling undone */
+    S->dual_uns = S->dual_inf / P->obj_scale;
+    double pu = 0.0;
+    for (int r = 0; r < m; ++r) pu = fmax(pu, fabs(S->cv[r] / (P->c_scale ? P->c_scale[r] : 1.0)));
+    S->prim_uns = pu;
+    S->compl_uns = S->compl0 / P->obj_scale;
+}
+
+/* OptimalityErrorConvergenceCheck::CurrentIsAcceptable (the objective-change bookkeeping
+ * runs once per iteration) */
+static int current_is_acceptable(ipm* S) {
+    const ora_ipm_opts* o = S->o;
+    if (*S->iter != S->last_obj_iter) {
+        S->last_obj = S->curr_obj;
+        S->curr_obj = S->f;
+        S->last_obj_iter = *S->iter;
+    }
+    return S->E0 <= o->acceptable_tol && S->dual_uns <= o->acceptable_dual_inf_tol &&
+           S->prim_uns <= o->acceptable_constr_viol_tol && S->compl_uns <= o->acceptable_compl_inf_tol &&
+           fabs(S->last_obj - S->curr_obj) / fmax(1.0, fabs(S->curr_obj)) <= o->acceptable_obj_change_tol;
+}
+
+/* --------------------------------------------------------------- the filter */
+static void filter_add(ipm* S, double ph, double th) {
+    /* Filter::AddEntry: drop the entries the new one dominates, then append */
+    int k = 0;
+    for (int i = 0; i < S->nf; ++i) {
+        int dominated = (ph <= S->fph[i]) && (th <= S->fth[i]);
+        if (!dominated) {
+            S->fph[k] = S->fph[i];
+            S->fth[k] = S->fth[i];
+            ++k;
+        }
+    }
+    S->nf = k;
+    if (S->nf == S->capf) {
+        S->capf *= 2;
+        S->fth = (double*)realloc(S->fth, sizeof(double) * S->capf);
+        S->fph = (double*)realloc(S->fph, sizeof(double) * S->capf);
+    }
+    S->fph[S->nf] = ph;
+    S->fth[S->nf] = th;
+    ++S->nf;
+}
+static int filter_acceptable(const ipm* S, double ph, double th) {
+    for (int i = 0; i < S->nf; ++i)
+        if (!(ph < S->fph[i] || th < S->fth[i])) return 0;
+    return 1;
+}
+static void augment_filter(ipm* S) {
+    const double gamma_theta = 1e-5, gamma_phi = 1e-8;
+    filter_add(S, S->ref_phi - gamma_phi * S->ref_theta, (1.0 - gamma_theta) * S->ref_theta);
+}
+static int is_ftype(const ipm* S, double alpha_test) {
+    const double delta = 1.0, s_theta = 1.1, s_phi = 2.3;
+    return S->ref_gd < 0.0 && alpha_test * pow(-S->ref_gd, s_phi) > delta * pow(S->ref_theta, s_theta);
+}
+static int armijo_holds(const ipm* S, double alpha_test, double phit) {
+    const double eta_phi = 1e-8;
+    return compare_le(phit - S->ref_phi, eta_phi * alpha_test * S->ref_gd, S->ref_phi);
+}
+static int acceptable_to_current_iterate(const ipm* S, double phit, double thetat, int from_resto) {
+    const double gamma_theta = 1e-5, gamma_phi = 1e-8;
+    if (!from_resto && phit > S->ref_phi) {
+        double basval = 1.0;
+        if (fabs(S->ref_phi) > 10.0) basval = log10(fabs(S->ref_phi));
+        if (log10(phit - S->ref_phi) > S->o->obj_max_inc * basval) return 0;
+    }
+    return compare_le(thetat, (1.0 - gamma_theta) * S->ref_theta, S->ref_theta) ||
+           compare_le(phit - S->ref_phi, -gamma_phi * S->ref_theta, S->ref_phi);
+}
+/* FilterLSAcceptor::CheckAcceptabilityOfTrialPoint */
+static int check_acceptability(ipm* S, double alpha_test, double phit, double thetat) {
+    if (S->theta_max < 0.0) S->theta_max = 1e4 * fmax(1.0, S->ref_theta);
+    if (S->theta_min < 0.0) S->theta_min = 1e-4 * fmax(1.0, S->ref_theta);
+    if (S->theta_max > 0 && thetat > S->theta_max) return 0;
+    int accept;
+    if (alpha_test > 0.0 && is_ftype(S, alpha_test) && S->ref_theta <= S->theta_min)
+        accept = armijo_holds(S, alpha_test, phit);
+    else
+        accept = acceptable_to_current_iterate(S, phit, thetat, 0);
+    if (!accept) {
+        S->last_rej_filter = 0;
+        return 0;
+    }
+    if (!filter_acceptable(S, phit, thetat)) {
+        S->last_rej_filter = 1;
+        return 0;
+    }
+    /* filter reset heuristic */
+    if (S->o->max_filter_resets > 0 && S->n_filter_resets < S->o->max_filter_resets) {
+        if (S->last_rej_filter) {
+            if (++S->count_filter_rej >= S->o->filter_reset_trigger) {
+                S->nf = 0;
+                S->count_filter_rej = 0;
+                ++S->n_filter_resets;
+            }
+        } else {
+            S->count_filter_rej = 0;
+        }
+    }
+    return 1;
+}
+/* FilterLSAcceptor::CalculateAlphaMin (on the reference point's values) */
+static double alpha_min_of(const ipm* S) {
+    const double gamma_theta = 1e-5, gamma_phi = 1e-8, delta = 1.0, s_theta = 1.1, s_phi = 2.3;
+    const double gBD = S->ref_gd, th = S->ref_theta;
+    double a;
+    if (gBD < 0) {
+        a = fmin(gamma_theta, gamma_phi * th / (-gBD));
+        if (th <= S->theta_min) a = fmin(a, delta * pow(th, s_theta) / pow(-gBD, s_phi));
+    } else {
+        a = gamma_theta;
+    }
+    return 0.05 * a;
+}
+
+/* ------------------------------------------------- the primal-dual system */
+/* Build and factor the KKT matrix of the current iterate with inertia correction
+ * (PDPerturbationHandler, Algorithm IC).  Returns 1 on success. */
+static int factor_kkt(ipm* S) {
+    iprob* P = S->P;
+    const int nw = S->nw, m = S->m, K = S->K;
+    P->hess(P, S->w, 1.0, S->mu, S->y, S->W);
+    double delta_w = 0.0, delta_c = 0.0;
+    int attempt = 0;
+    for (;;) {
+        memset(S->KKT, 0, sizeof(double) * (size_t)K * K);
+        for (int j = 0; j < nw; ++j)
+            for (int i = j; i < nw; ++i) S->KKT[i + (size_t)j * K] = S->W[(size_t)i * nw + j];
+        for (int i = 0; i < nw; ++i) {
+            double sig = 0.0;
+            if (P->hasL[i]) sig += S->zL[i] / (S->w[i] - P->wl[i]);
+            if (P->hasU[i]) sig += S->zU[i] / (P->wu[i] - S->w[i]);
+            S->KKT[i + (size_t)i * K] += sig + delta_w;
+        }
+        for (int r = 0; r < m; ++r) {
+            for (int j = 0; j < nw; ++j) S->KKT[(nw + r) + (size_t)j * K] = S->A[(size_t)r * nw + j];
+            S->KKT[(nw + r) + (size_t)(nw + r) * K] = -delta_c;
+        }
+        int np, nn, nz;
+        ora_ldlt_factor(K, S->KKT, S->ipiv, 1e-300, &np, &nn, &nz);
+        if (np == nw && nn == m && nz == 0) {
+            if (delta_w > 0) S->dw_last = delta_w;
+            return 1;
+        }
+        if (nz > 0 && delta_c == 0.0) delta_c = 1e-8 * pow(S->mu, 0.25);
+        if (attempt == 0)
+            delta_w = (S->dw_last == 0.0) ? 1e-4 : fmax(1e-20, S->dw_last / 3.0);
+        else
+            delta_w = (S->dw_last == 0.0) ? 100.0 * delta_w : 8.0 * delta_w;
+        ++attempt;
+        if (delta_w > 1e40) return 0;
+    }
+}
+/* Solve the factored system for the step with constraint right-hand side -crhs; the
+ * stationarity rows carry the barrier gradient (Ipopt's grad_lag_with_damping plus the
+ * relaxed complementarity, eliminated).  z steps from the complementarity rows. */
+static void solve_step(ipm* S, const double* crhs, double* dw, double* dy, double* dzL, double* dzU) {
+    iprob* P = S->P;
+    const int nw = S->nw, m = S->m;
+    for (int i = 0; i < nw; ++i) {
+        double s = S->gphi[i];
+        for (int r = 0; r < m; ++r) s += S->A[(size_t)r * nw + i] * S->y[r];
+        S->rhs[i] = -s;
+    }
+    for (int r = 0; r < m; ++r) S->rhs[nw + r] = -crhs[r];
+    ora_ldlt_solve(S->K, S->KKT, S->ipiv, S->rhs);
+    for (int i = 0; i < nw; ++i) dw[i] = S->rhs[i];
+    for (int r = 0; r < m; ++r) dy[r] = S->rhs[nw + r];
+    for (int i = 0; i < nw; ++i) {
+        dzL[i] = P->hasL[i] ? S->mu / (S->w[i] - P->wl[i]) - S->zL[i] - S->zL[i] / (S->w[i] - P->wl[i]) * dw[i] : 0.0;
+        dzU[i] = P->hasU[i] ? S->mu / (P->wu[i] - S->w[i]) - S->zU[i] + S->zU[i] / (P->wu[i] - S->w[i]) * dw[i] : 0.0;
+    }
+}
+static double primal_frac(const ipm* S, const double* w, const double* dw) {
+    iprob* P = S->P;
+    double a = 1.0;
+    for (int i = 0; i < S->nw; ++i) {
+        if (P->hasL[i] && dw[i] < 0) a = fmin(a, -S->tau * (w[i] - P->wl[i]) / dw[i]);
+        if (P->hasU[i] && dw[i] > 0) a = fmin(a, S->tau * (P->wu[i] - w[i]) / dw[i]);
+    }
+    return a;
+}
+static double dual_frac(const ipm* S, const double* zL, const double* zU, const double* dzL, const double* dzU) {
+    iprob* P = S->P;
+    double a = 1.0;
+    for (int i = 0; i < S->nw; ++i) {
+        if (P->hasL[i] && dzL[i] < 0) a = fmin(a, -S->tau * zL[i] / dzL[i]);
+        if (P->hasU[i] && dzU[i] < 0) a = fmin(a, -S->tau * zU[i] / dzU[i]);
+    }
+    return a;
+}
+
+/* trial primal point w + alpha d: phi, theta (c at the trial point in S->ct); ok = 0 on an
+ * evaluation error (outside the bounds, non-finite) */
+static int eval_trial(ipm* S, double alpha, const double* d, double* phit, double* thetat) {
+    for (int i = 0; i < S->nw; ++i) S->wt[i] = S->w[i] + alpha * d[i];
+    int ok;
+    *phit = barrier_phi(S, S->wt, &ok);
+    S->P->cons(S->P, S->wt, S->ct);
+    *thetat = l1(S->m, S->ct);
+    return ok && isfinite(*thetat);
+}
+/* PerformDualStep: z with alpha_dual, y with the primal step length (alpha_for_y primal) */
+static void dual_step(ipm* S, double alpha_p, double alpha_d, const double* dy, const double* dzL,
+                      const double* dzU) {
+    for (int r = 0; r < S->m; ++r) S->yt[r] = S->y[r] + alpha_p * dy[r];
+    for (int i = 0; i < S->nw; ++i) {
+        S->zLt[i] = S->zL[i] + alpha_d * dzL[i];
+        S->zUt[i] = S->zU[i] + alpha_d * dzU[i];
+    }
+}
+static void copy_dir(ipm* S, double* w, double* y, double* zL, double* zU, const double* w2, const double* y2,
+                     const double* zL2, const double* zU2) {
+    memcpy(w, w2, sizeof(double) * S->nw);
+    memcpy(y, y2, sizeof(double) * S->m);
+    memcpy(zL, zL2, sizeof(double) * S->nw);
+    memcpy(zU, zU2, sizeof(double) * S->nw);
+}
+
+/* FilterLSAcceptor::TrySecondOrderCorrection */
+static int try_soc(ipm* S, double alpha_test, double* alpha, double theta_trial) {
+    const ora_ipm_opts* o = S->o;
+    if (o->max_soc <= 0) return 0;
+    int count = 0, accept = 0;
+    double theta_old = 0.0, alpha_soc = *alpha;
+    memcpy(S->csoc, S->cv, sizeof(double) * S->m);
+    double* sw = (double*)malloc(sizeof(double) * (2 * S->nw + S->nw + S->m));
+    double *dzl = sw, *dzu = sw + S->nw, *dws = sw + 2 * S->nw, *dys = dws + S->nw;
+    while (count < o->max_soc && !accept && (count == 0 || theta_trial <= o->kappa_soc * theta_old)) {
+        theta_old = theta_trial;
+        for (int r = 0; r < S->m; ++r) S->csoc[r] = S->ct[r] + alpha_soc * S->csoc[r];
+        solve_step(S, S->csoc, dws, dys, dzl, dzu);
+        alpha_soc = primal_frac(S, S->w, dws);
+        double phit, thetat;
+        int ok = eval_trial(S, alpha_soc, dws, &phit, &thetat);
+        accept = ok && check_acceptability(S, alpha_test, phit, thetat);
+        if (accept) {
+            *alpha = alpha_soc;
+            copy_dir(S, S->aw, S->ay, S->azL, S->azU, dws, dys, dzl, dzu);
+            if (S->diag) ++S->diag->n_soc;
+        } else {
+            ++count;
+            theta_trial = thetat;
+        }
+    }
+    free(sw);
+    return accept;
+}
+
+/* BacktrackingLineSearch::DoBacktrackingLineSearch on the actual step (aw, ...). */
+static int backtracking(ipm* S, int skip_first, double* alpha_out, int* n_steps, int* eval_error) {
+    *eval_error = 0;
+    const double alpha_max = primal_frac(S, S->w, S->aw);
+    const double alpha_min = S->in_wd ? alpha_max : alpha_min_of(S);
+    double alpha = alpha_max;
+    double alpha_test = S->in_wd ? S->wd_alpha_test : alpha;
+    if (skip_first) alpha *= 0.5;
+    int accept = 0;
+    *n_steps = 0;
+    while (alpha > alpha_min || *n_steps == 0) {
+        double phit, thetat;
+        int ok = eval_trial(S, alpha, S->aw, &phit, &thetat);
+        if (!S->in_wd) alpha_test = alpha;
+        if (ok) {
+            accept = check_acceptability(S, alpha_test, phit, thetat);
+        } else {
+            accept = 0;
+            *eval_error = 1;
+        }
+        if (accept) {
+            /* UpdateForNextIteration: augment unless an f-type step with Armijo */
+            if (!is_ftype(S, alpha_test) || !armijo_holds(S, alpha_test, phit)) augment_filter(S);
+            break;
+        }
+        if (S->in_wd) break;
+        if (!*eval_error && alpha == alpha_max && S->theta <= thetat) {
+            accept = try_soc(S, alpha_test, &alpha, thetat);
+            if (accept) {
+                /* the SOC trial point is in wt; its filter bookkeeping as above */
+                double phis;
+                int oks;
+                phis = barrier_phi(S, S->wt, &oks);
+                if (!is_ftype(S, alpha_test) || !armijo_holds(S, alpha_test, phis)) augment_filter(S);
+                break;
+            }
+        }
+        alpha *= 0.5;
+        ++*n_steps;
+    }
+    *alpha_out = alpha;
+    return accept;
+}
+
+static void start_watchdog(ipm* S) {
+    S->in_wd = 1;
+    copy_dir(S, S->wd_w, S->wd_y, S->wd_zL, S->wd_zU, S->w, S->y, S->zL, S->zU);
+    copy_dir(S, S->wd_dw, S->wd_dy, S->wd_dzL, S->wd_dzU, S->dw, S->dy, S->dzL, S->dzU);
+    S->wd_trial_iter = 0;
+    S->wd_alpha_test = primal_frac(S, S->w, S->dw);
+    S->wd_theta = S->ref_theta;
+    S->wd_phi = S->ref_phi;
+    S->wd_gd = S->ref_gd;
+    if (S->diag) ++S->diag->n_watchdog;
+}
+static void stop_watchdog(ipm* S) {
+    S->in_wd = 0;
+    copy_dir(S, S->w, S->y, S->zL, S->zU, S->wd_w, S->wd_y, S->wd_zL, S->wd_zU);
+    copy_dir(S, S->aw, S->ay, S->azL, S->azU, S->wd_dw, S->wd_dy, S->wd_dzL, S->wd_dzU);
+    S->ref_theta = S->wd_theta;
+    S->ref_phi = S->wd_phi;
+    S->ref_gd = S->wd_gd;
+    S->wd_short = 0;
+    /* the current iterate is the restored one */
+    eval_current(S);
+    int ok;
+    S->phi = barrier_phi(S, S->w, &ok);
+}
+
+/* primal-dual system error of (w, y, zL, zU) for the soft restoration phase
+ * (curr_primal_dual_system_error: 1-norms of the dual infeasibility, the constraint
+ * violation and the mu-complementarity, averaged over all their entries) */
+static double pd_error(ipm* S, const double* w, const double* y, const double* zL, const double* zU, int trial) {
+    iprob* P = S->P;
+    double *g = trial ? S->gft : S->gf, *A = trial ? S->At : S->A, *rd = trial ? S->rdt : S->rd;
+    double *c = trial ? S->ct : S->cv;
+    if (trial) {
+        P->grad(P, w, S->mu, g);
+        P->jac(P, w, A);
+        P->cons(P, w, c);
+    }
+    lag_grad(S, g, A, y, zL, zU, rd);
+    const double du = l1(S->nw, rd), pr = l1(S->m, c), cm = compl_norm(S, w, zL, zU, S->mu, 1);
+    return (du + pr + cm) / (double)(S->nw + S->m + S->nbnd);
+}
+/* BacktrackingLineSearch::TrySoftRestoStep */
+static int try_soft_resto(ipm* S, int* satisfies_orig) {
+    *satisfies_orig = 0;
+    const double ap = primal_frac(S, S->w, S->aw);
+    const double ad = dual_frac(S, S->zL, S->zU, S->azL, S->azU);
+    const double a = fmin(ap, ad);
+    double phit, thetat;
+    int ok = eval_trial(S, a, S->aw, &phit, &thetat);
+    dual_step(S, a, a, S->ay, S->azL, S->azU);
+    if (!ok) return 0;
+    if (check_acceptability(S, 0.0, phit, thetat)) {
+        *satisfies_orig = 1;
+        if (S->diag) ++S->diag->n_soft_resto;
+        return 1;
+    }
+    const double et = pd_error(S, S->wt, S->yt, S->zLt, S->zUt, 1);
+    const double ec = pd_error(S, S->w, S->y, S->zL, S->zU, 0);
+    if (et <= S->o->soft_resto_pderror_reduction_factor * ec) {
+        if (S->diag) ++S->diag->n_soft_resto;
+        return 1;
+    }
+    return 0;
+}
+
+static int ipm_iterate(ipm* S);
+
+/* MinC_1NrmRestorationPhase::PerformRestoration.  On success the trial point (wt, yt,
+ * zLt, zUt) holds the point to continue from and 0 is returned; otherwise a status. */
+static int perform_restoration(ipm* S) {
+    iprob* P = S->P;
+    const int nx = S->nw, m = S->m, nv = nx + 2 * m;
+    if (S->diag) ++S->diag->n_resto;
+    resto_ctx rc;
+    rc.orig = P;
+    rc.nx = nx;
+    rc.m = m;
+    rc.rho = 1000.0;
+    double* buf = (double*)calloc((size_t)2 * nx + m + (size_t)m * nx + 2 * nv + 2 * nv, sizeof(double));
+    double *xR = buf, *DR = xR + nx;
+    rc.c = DR + nx;
+    rc.A = rc.c + m;
+    double *vl = rc.A + (size_t)m * nx, *vu = vl + nv;
+    char* hb = (char*)calloc(2 * nv, 1);
+    for (int i = 0; i < nx; ++i) {
+        xR[i] = S->w[i];
+        DR[i] = 1.0 / fmax(1.0, fabs(S->w[i]));
+    }
+    rc.xR = xR;
+    rc.DR = DR;
+    iprob R;
+    memset(&R, 0, sizeof R);
+    R.nw = nv;
+    R.m = m;
+    R.ctx = &rc;
+    R.f = resto_f;
+    R.grad = resto_grad;
+    R.cons = resto_cons;
+    R.jac = resto_jac;
+    R.hess = resto_hess;
+    R.wl = vl;
+    R.wu = vu;
+    R.hasL = hb;
+    R.hasU = hb + nv;
+    R.obj_scale = 1.0;
+    R.c_scale = NULL;
+    for (int i = 0; i < nx; ++i) {
+        vl[i] = P->wl[i];
+        vu[i] = P->wu[i];
+        R.hasL[i] = P->hasL[i];
+        R.hasU[i] = P->hasU[i];
+    }
+    for (int i = nx; i < nv; ++i) {
+        vl[i] = 0.0;
+        vu[i] = INFINITY;
+        R.hasL[i] = 1;
+        R.hasU[i] = 0;
+    }
+    ipm Rs;
+    ipm_alloc(&Rs, &R, S->o);
+    Rs.is_resto = 1;
+    Rs.outer = S;
+    Rs.iter = S->iter;
+    Rs.diag = NULL;
+    Rs.resto_first = 1;
+    /* RestoIterateInitializer: mu_R = max(mu, ||c||_inf), p and n the minimisers of the
+     * l1 penalty with barrier for fixed x, x bound multipliers min(rho, z), p/n
+     * multipliers mu_R / p, mu_R / n, y = 0 */
+    const double muR = fmax(S->mu, amax(m, S->cv));
+    Rs.mu = muR;
+    Rs.tau = fmax(0.99, 1.0 - muR);
+    for (int i = 0; i < nx; ++i) {
+        Rs.w[i] = S->w[i];
+        Rs.zL[i] = P->hasL[i] ? fmin(rc.rho, S->zL[i]) : 0.0;
+        Rs.zU[i] = P->hasU[i] ? fmin(rc.rho, S->zU[i]) : 0.0;
+    }
+    for (int r = 0; r < m; ++r) {
+        const double c = S->cv[r];
+        const double a = muR / (2.0 * rc.rho) - 0.5 * c, b = c * muR / (2.0 * rc.rho);
+        const double nn = a + sqrt(a * a + b), pp = c + nn;
+        Rs.w[nx + r] = pp;
+        Rs.w[nx + m + r] = nn;
+        Rs.zL[nx + r] = muR / pp;
+        Rs.zL[nx + m + r] = muR / nn;
+        Rs.y[r] = 0.0;
+    }
+    const int it0 = *S->iter;
+    int st = ipm_iterate(&Rs);
+    if (S->diag) S->diag->resto_iters += *S->iter - it0;
+    if (st == 0) {
+        /* back to the original problem: x from the restoration phase, y = 0
+         * (constr_mult_reset_threshold 0), bound multipliers by a Newton step of the
+         * complementarity with the whole restoration step as the primal step
+         * (ComputeBoundMultiplierStep), reset to 1 above bound_mult_reset_threshold */
+        for (int i = 0; i < nx; ++i) S->wt[i] = Rs.w[i];
+        for (int r = 0; r < m; ++r) S->yt[r] = 0.0;
+        double* dz = (double*)malloc(sizeof(double) * 2 * nx);
+        for (int i = 0; i < nx; ++i) {
+            double dl = 0.0, du = 0.0;
+            if (P->hasL[i]) {
+                const double sc = S->w[i] - P->wl[i], st_ = S->wt[i] - P->wl[i];
+                dl = (S->mu + S->zL[i] * (sc - st_)) / sc - S->zL[i];
+            }
+            if (P->hasU[i]) {
+                const double sc = P->wu[i] - S->w[i], st_ = P->wu[i] - S->wt[i];
+                du = (S->mu + S->zU[i] * (sc - st_)) / sc - S->zU[i];
+            }
+            dz[i] = dl;
+            dz[nx + i] = du;
+        }
+        const double ad = dual_frac(S, S->zL, S->zU, dz, dz + nx);
+        double zmax = 0.0;
+        for (int i = 0; i < nx; ++i) {
+            S->zLt[i] = S->zL[i] + ad * dz[i];
+            S->zUt[i] = S->zU[i] + ad * dz[nx + i];
+            zmax = fmax(zmax, fmax(fabs(S->zLt[i]), fabs(S->zUt[i])));
+        }
+        if (zmax > 1000.0)
+            for (int i = 0; i < nx; ++i) {
+                S->zLt[i] = P->hasL[i] ? 1.0 : 0.0;
+                S->zUt[i] = P->hasU[i] ? 1.0 : 0.0;
+            }
+        free(dz);
+    }
+    ipm_free(&Rs);
+    free(buf);
+    free(hb);
+    return st;
+}
+
+/* BacktrackingLineSearch::FindAcceptableTrialPoint.  Returns 0 with the accepted trial
+ * point in (wt, yt, zLt, zUt), or a termination status. */
+static int find_trial_point(ipm* S, int goto_resto) {
+    const ora_ipm_opts* o = S->o;
+    if (S->mu != S->last_mu) {
+        S->in_wd = 0;
+        S->wd_short = 0;
+        S->last_mu = S->mu;
+    }
+    if (!S->is_resto && o->acceptable_iter > 0 && current_is_acceptable(S)) {
+        copy_dir(S, S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->w, S->y, S->zL, S->zU);
+        S->have_acc = 1;
+    }
+    copy_dir(S, S->aw, S->ay, S->azL, S->azU, S->dw, S->dy, S->dzL, S->dzU);
+    if (!goto_resto) {
+        /* InitThisLineSearch */
+        if (S->in_wd) {
+            S->ref_theta = S->wd_theta;
+            S->ref_phi = S->wd_phi;
+            S->ref_gd = S->wd_gd;
+        } else {
+            S->ref_theta = S->theta;
+            S->ref_phi = S->phi;
+            S->ref_gd = S->gd;
+        }
+    }
+    int accept = 0, n_steps = 0, soft_or_resto = 0;
+    double alpha = 0.0;
+    /* DetectTinyStep */
+    int tiny = 0;
+    if (!goto_resto && o->tiny_step_tol > 0) {
+        double rel = 0.0;
+        for (int i = 0; i < S->nw; ++i) rel = fmax(rel, fabs(S->dw[i]) / (1.0 + fabs(S->w[i])));
+        tiny = rel <= o->tiny_step_tol && (S->m == 0 || amax(S->m, S->dy) <= o->tiny_step_y_tol);
+    }
+    if (S->in_wd && (goto_resto || tiny)) {
+        stop_watchdog(S);
+        goto_resto = 0;
+        tiny = 0;
+    }
+    if (o->watchdog_shortened_iter_trigger > 0 && !S->in_wd && !goto_resto && !tiny && !S->in_soft &&
+        S->wd_short >= o->watchdog_shortened_iter_trigger)
+        start_watchdog(S);
+    if (tiny) {
+        alpha = primal_frac(S, S->w, S->dw);
+        double phit, thetat;
+        eval_trial(S, alpha, S->dw, &phit, &thetat);
+        if (S->tiny_last) S->tiny_flag = 1;
+        S->tiny_last = 1;
+        accept = 1;
+    } else {
+        S->tiny_last = 0;
+    }
+    if (!goto_resto && !tiny) {
+        if (S->in_soft) {
+            if (++S->soft_count > o->max_soft_resto_iters) {
+                accept = 0;
+            } else {
+                int sat;
+                accept = try_soft_resto(S, &sat);
+                if (accept && sat) {
+                    S->in_soft = 0;
+                    S->soft_count = 0;
+                }
+            }
+            soft_or_resto = accept;
+        } else {
+            int done = 0, skip_first = 0, eval_error;
+            while (!done) {
+                accept = backtracking(S, skip_first, &alpha, &n_steps, &eval_error);
+                if (S->in_wd) {
+                    if (accept) {
+                        S->in_wd = 0;
+                        done = 1;
+                    } else {
+                        ++S->wd_trial_iter;
+                        if (eval_error || S->wd_trial_iter > o->watchdog_trial_iter_max) {
+                            stop_watchdog(S);
+                            skip_first = 1;
+                        } else {
+                            done = 1;
+                            accept = 1;
+                        }
+                    }
+                } else {
+                    done = 1;
+                }
+            }
+        }
+    }
+    if (!accept) {
+        if (!S->in_soft && o->soft_resto_pderror_reduction_factor > 0.0 && !goto_resto) {
+            augment_filter(S); /* PrepareRestoPhaseStart */
+            int sat;
+            if (try_soft_resto(S, &sat)) {
+                S->in_soft = !sat;
+                accept = 1;
+                soft_or_resto = 1;
+            }
+        }
+        if (!accept) {
+            if (!S->in_soft) augment_filter(S);
+            if (S->is_resto || !o->restoration || S->m == 0) return ORA_RESTORATION_FAILURE;
+            /* almost feasible: restore the stored acceptable point, if any */
+            if (S->theta <= 1e-2 * o->tol) {
+                if (S->have_acc) {
+                    copy_dir(S, S->w, S->y, S->zL, S->zU, S->acc_w, S->acc_y, S->acc_zL, S->acc_zU);
+                    return ORA_STOP_AT_ACCEPTABLE_POINT;
+                }
+                return ORA_RESTORATION_FAILURE;
+            }
+            if (((orig_ctx*)S->P->ctx)->mI > 0) return ORA_RESTORATION_FAILURE;
+            S->in_soft = 0;
+            S->soft_count = 0;
+            S->wd_short = 0;
+            int st = perform_restoration(S);
+            if (st) return st;
+            return 0; /* trial point set by the restoration phase (no dual step here) */
+        }
+    }
+    if (!soft_or_resto) {
+        /* dual step of the accepted primal step and the watchdog counter */
+        const double ad = dual_frac(S, S->zL, S->zU, S->azL, S->azU);
+        dual_step(S, alpha, ad, S->ay, S->azL, S->azU);
+        if (n_steps == 0)
+            S->wd_short = 0;
+        else
+            ++S->wd_short;
+    }
+    return 0;
+}
+
+/* IpoptAlgorithm::AcceptTrialPoint: bound multipliers kept within kappa_sigma of mu / s */
+static void accept_trial(ipm* S) {
+    iprob* P = S->P;
+    const double ks = 1e10, mu = S->mu;
+    memcpy(S->w, S->wt, sizeof(double) * S->nw);
+    memcpy(S->y, S->yt, sizeof(double) * S->m);
+    for (int i = 0; i < S->nw; ++i) {
+        if (P->hasL[i]) {
+            const double s = S->w[i] - P->wl[i];
+            S->zL[i] = fmax(fmin(S->zLt[i], ks * mu / s), mu / (ks * s));
+        } else {
+            S->zL[i] = 0.0;
+        }
+        if (P->hasU[i]) {
+            const double s = P->wu[i] - S->w[i];
+            S->zU[i] = fmax(fmin(S->zUt[i], ks * mu / s), mu / (ks * s));
+        } else {
+            S->zU[i] = 0.0;
+        }
+    }
+}
+
+/* convergence check of the restoration problem (RestoConvergenceCheck +
+ * RestoFilterConvergenceCheck::TestOrigProgress).  Returns -1 to continue, 0 when the
+ * original problem can take over, or a status. */
+static int resto_convergence(ipm* S) {
+    ipm* O = S->outer;
+    const ora_ipm_opts* o = S->o;
+    int status = -1;
+    if (S->resto_first) {
+        S->resto_first = 0;
+    } else {
+        int ok;
+        const double bt = barrier_phi(O, S->w, &ok);
+        O->P->cons(O->P, S->w, O->ct);
+        const double tt = l1(O->m, O->ct);
+        if (ok && isfinite(tt) && tt <= 0.9 * O->theta && filter_acceptable(O, bt, tt) &&
+            acceptable_to_current_iterate(O, bt, tt, 1))
+            status = 0;
+    }
+    if (status < 0) {
+        /* the restoration problem's own optimality */
+        if (S->E0 <= o->tol && S->dual_uns <= 1.0 && S->prim_uns <= 1e-4 && S->compl_uns <= 1e-4) {
+            O->P->cons(O->P, S->w, O->ct);
+            return amax(O->m, O->ct) <= 1e2 * o->tol ? ORA_FEASIBLE_POINT_FOUND : ORA_LOCAL_INFEASIBILITY;
+        }
+        if (*S->iter >= o->max_iter) return ORA_MAXITER_EXCEEDED;
+        if (o->cpu_iter_budget >= 0 && *S->iter > o->cpu_iter_budget) return ORA_UNKNOWN;
+    }
+    return status;
+}
+
+/* The main loop (IpoptAlgorithm::Optimize).  Returns a status, or (restoration problem) 0
+ * when the original problem can take over. */
+static int ipm_iterate(ipm* S) {
+    const ora_ipm_opts* o = S->o;
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+    const double mu_min = fmin(o->tol, 1e-4) / (kappa_eps + 1.0);
+    for (;;) {
+        eval_current(S);
+        {
+            int okp;
+            S->phi = barrier_phi(S, S->w, &okp);
+        }
+        if (o->print_level > 0)
+            fprintf(stderr, "%s%3d mu %.2e E0 %.3e dual %.3e prim %.3e compl %.3e th %.3e f %.10e nf %d\n",
+                    S->is_resto ? "r" : "", *S->iter, S->mu, S->E0, S->dual_inf, S->prim_inf, S->compl0, S->theta,
+                    S->f, S->nf);
+        /* Ipopt's finiteness test of f and g at an evaluated point (OrigIpoptNLP) ->
+         * INVALID_NUMBER_DETECTED: amax() drops a NaN, the l1 norm and f do not */
+        if (!isfinite(S->E0) || !isfinite(S->theta) || !isfinite(S->f)) return ORA_INVALID_NUMBER_DETECTED;
+        /* ---- convergence (OptimalityErrorConvergenceCheck::CheckConvergence) ---- */
+        if (S->is_resto) {
+            int st = resto_convergence(S);
+            if (st >= 0) return st;
+        } else {
+            if (S->E0 <= o->tol && S->dual_uns <= 1.0 && S->prim_uns <= 1e-4 && S->compl_uns <= 1e-4)
+                return ORA_SUCCESS;
+            if (o->acceptable_iter > 0 && current_is_acceptable(S)) {
+                if (++S->acc_counter >= o->acceptable_iter) return ORA_STOP_AT_ACCEPTABLE_POINT;
+            } else {
+                S->acc_counter = 0;
+            }
+            if (*S->iter >= o->max_iter) return ORA_MAXITER_EXCEEDED;
+            if (o->cpu_iter_budget >= 0 && *S->iter > o->cpu_iter_budget) return ORA_UNKNOWN;
+        }
+        /* ---- monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter) ---- */
+        {
+            int tiny_flag = S->tiny_flag;
+            S->tiny_flag = 0;
+            int done = 0;
+            double complmu = compl_norm(S, S->w, S->zL, S->zU, S->mu, 0);
+            double Emu = fmax(S->dual_inf / S->sd, fmax(S->prim_inf, complmu / S->sc));
+            while ((Emu <= kappa_eps * S->mu || tiny_flag) && !done) {
+                double mnew = fmax(fmin(kappa_mu * S->mu, pow(S->mu, theta_mu)), mu_min);
+                int changed = mnew != S->mu;
+                if (!changed && tiny_flag) return ORA_STOP_AT_TINY_STEP;
+                S->mu = mnew;
+                S->tau = fmax(0.99, 1.0 - mnew);
+                if (!changed) {
+                    done = 1;
+                } else {
+                    if (S->is_resto) eval_current(S); /* the restoration objective depends on mu */
+                    complmu = compl_norm(S, S->w, S->zL, S->zU, S->mu, 0);
+                    Emu = fmax(S->dual_inf / S->sd, fmax(S->prim_inf, complmu / S->sc));
+                    done = Emu > kappa_eps * S->mu;
+                }
+                if (done && changed) {
+                    /* BacktrackingLineSearch::Reset */
+                    S->in_soft = 0;
+                    S->in_wd = 0;
+                    S->wd_short = 0;
+                    S->nf = 0;
+                }
+                tiny_flag = 0;
+            }
+        }
+        /* the barrier function changed with mu */
+        if (S->is_resto) {
+            /* the restoration objective depends on mu (eta = sqrt(mu)) */
+            eval_current(S);
+        }
+        {
+            int okp;
+            S->phi = barrier_phi(S, S->w, &okp);
+        }
+        /* ---- search direction ---- */
+        barrier_grad(S, S->w, S->gf, S->gphi);
+        int goto_resto = 0;
+        if (factor_kkt(S)) {
+            solve_step(S, S->cv, S->dw, S->dy, S->dzL, S->dzU);
+        } else {
+            if (S->is_resto || !o->restoration) return ORA_ERROR_IN_STEP_COMPUTATION;
+            goto_resto = 1; /* fallback: restoration phase */
+            memset(S->dw, 0, sizeof(double) * S->nw);
+            memset(S->dy, 0, sizeof(double) * S->m);
+            memset(S->dzL, 0, sizeof(double) * S->nw);
+            memset(S->dzU, 0, sizeof(double) * S->nw);
+        }
+        S->gd = 0.0;
+        for (int i = 0; i < S->nw; ++i) S->gd += S->gphi[i] * S->dw[i];
+        /* ---- line search ---- */
+        int st = find_trial_point(S, goto_resto);
+        if (st) return st;
+        accept_trial(S);
+        ++*S->iter;
+    }
+}
+
+int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out, double* zl_out, double* zu_out,
+                  double* lambda_out, double* g_out, ora_ipm_result* res) {
     ora_ipm_opts opts;
     if (opts_in) opts = *opts_in; else ora_ipm_default_opts(&opts);
     const int n = nlp->n, m = nlp->m;
-    ipm_ctx C;
-    memset(&C, 0, sizeof C);
-    C.nlp = nlp;
-    C.n = n;
-    C.m = m;
-    C.ineq_of_row = (int*)malloc(sizeof(int) * (m > 0 ? m : 1));
+    orig_ctx oc;
+    memset(&oc, 0, sizeof oc);
+    oc.nlp = nlp;
+    oc.n = n;
+    oc.m = m;
+    oc.ineq_of_row = (int*)malloc(sizeof(int) * (m > 0 ? m : 1));
     int mI = 0;
-    for (int r = 0; r < m; ++r) {
-        if (nlp->gl[r] == nlp->gu[r]) C.ineq_of_row[r] = -1;
-        else C.ineq_of_row[r] = mI++;
-    }
-    C.mI = mI;
+    for (int r = 0; r < m; ++r) oc.ineq_of_row[r] = (nlp->gl[r] == nlp->gu[r]) ? -1 : mI++;
+    oc.mI = mI;
     const int nw = n + mI;
-    C.nw = nw;
-    const int K = nw + m;
-    double* mem = (double*)calloc((size_t)(
-        20 * nw + 10 * m + (size_t)m * n + (size_t)n * n + (size_t)m * nw + (size_t)K * K + 4 * K + 16), sizeof(double));
-    double* p = mem;
-#define TAKE(ptr, cnt) do { ptr = p; p += (cnt); } while (0)
-    double *w, *wt, *y, *zL, *zU, *dw, *dy, *dzL, *dzU, *gf, *gphi, *cv, *ct, *rd, *A, *W, *KKT, *rhs, *wl0, *wu0;
-    TAKE(w, nw); TAKE(wt, nw); TAKE(y, m); TAKE(zL, nw); TAKE(zU, nw); TAKE(dw, nw); TAKE(dy, m);
-    TAKE(dzL, nw); TAKE(dzU, nw); TAKE(gf, nw); TAKE(gphi, nw); TAKE(cv, m); TAKE(ct, m); TAKE(rd, nw);
-    TAKE(A, (size_t)m * nw); TAKE(W, (size_t)n * n); TAKE(KKT, (size_t)K * K); TAKE(rhs, K);
-    TAKE(wl0, nw); TAKE(wu0, nw);
-    TAKE(C.wl, nw); TAKE(C.wu, nw); TAKE(C.gv, m); TAKE(C.jac, (size_t)m * n); TAKE(C.lam_unscaled, m);
-    TAKE(C.c_scale, m);
-#undef TAKE
-    int* ipiv = (int*)malloc(sizeof(int) * K);
-    C.hasL = (char*)calloc(nw, 1);
-    C.hasU = (char*)calloc(nw, 1);
-    int nfilter = 0, capfilter = 256;
-    fpair* filter = (fpair*)malloc(sizeof(fpair) * capfilter);
+    double* buf = (double*)calloc((size_t)6 * nw + 3 * m + (size_t)m * n + (size_t)n * n + 8, sizeof(double));
+    double *wl0 = buf, *wu0 = wl0 + nw, *wl = wu0 + nw, *wu = wl + nw, *gf0 = wu + nw;
+    oc.c_scale = gf0 + nw;
+    oc.gv = oc.c_scale + m;
+    oc.lam = oc.gv + m;
+    oc.jac = oc.lam + m;
+    oc.H = oc.jac + (size_t)m * n;
+    char* hb = (char*)calloc(2 * (size_t)nw + 2, 1);
+    iprob P;
+    memset(&P, 0, sizeof P);
+    P.nw = nw;
+    P.m = m;
+    P.ctx = &oc;
+    P.f = orig_f;
+    P.grad = orig_grad;
+    P.cons = orig_cons;
+    P.jac = orig_jac;
+    P.hess = orig_hess;
+    P.wl = wl;
+    P.wu = wu;
+    P.hasL = hb;
+    P.hasU = hb + nw;
+    P.c_scale = oc.c_scale;
 
-    /* ---- bounds on w (original), then relaxation (Ipopt bound_relax_factor) ---- */
+    /* ---- bounds on w (original), then relaxation (bound_relax_factor) ---- */
     for (int i = 0; i < n; ++i) { wl0[i] = nlp->xl[i]; wu0[i] = nlp->xu[i]; }
     for (int r = 0; r < m; ++r) {
-        int s = C.ineq_of_row[r];
+        int s = oc.ineq_of_row[r];
         if (s >= 0) { wl0[n + s] = nlp->gl[r]; wu0[n + s] = nlp->gu[r]; }
     }
     for (int i = 0; i < nw; ++i) {
-        C.hasL[i] = wl0[i] > -INF_BOUND;
-        C.hasU[i] = wu0[i] < INF_BOUND;
+        P.hasL[i] = wl0[i] > -INF_BOUND;
+        P.hasU[i] = wu0[i] < INF_BOUND;
         double rl = fmin(1e-4, opts.bound_relax_factor * fmax(1.0, fabs(wl0[i])));
         double ru = fmin(1e-4, opts.bound_relax_factor * fmax(1.0, fabs(wu0[i])));
-        C.wl[i] = C.hasL[i] ? wl0[i] - rl : -INFINITY;
-        C.wu[i] = C.hasU[i] ? wu0[i] + ru : INFINITY;
+        wl[i] = P.hasL[i] ? wl0[i] - rl : -INFINITY;
+        wu[i] = P.hasU[i] ? wu0[i] + ru : INFINITY;
     }
-
-    /* ---- starting point: x0 pushed inside (bound_push/bound_frac 0.01) ---- */
-    for (int i = 0; i < n; ++i) w[i] = nlp->x0[i];
-    /* gradient-based scaling at the user's starting point */
+    /* ---- gradient-based scaling at the user's starting point ---- */
     {
-        nlp->grad_f(nlp->ctx, w, gf);
-        double gmax = amax(n, gf);
-        C.obj_scale = (gmax > 100.0) ? 100.0 / gmax : 1.0;
-        nlp->jac_g(nlp->ctx, w, C.jac);
+        nlp->grad_f(nlp->ctx, nlp->x0, gf0);
+        double gmax = amax(n, gf0);
+        oc.obj_scale = (gmax > 100.0) ? 100.0 / gmax : 1.0;
+        nlp->jac_g(nlp->ctx, nlp->x0, oc.jac);
         for (int r = 0; r < m; ++r) {
-            double rm = amax(n, C.jac + (size_t)r * n);
-            C.c_scale[r] = (rm > 100.0) ? 100.0 / rm : 1.0;
+            double rm = amax(n, oc.jac + (size_t)r * n);
+            oc.c_scale[r] = (rm > 100.0) ? 100.0 / rm : 1.0;
         }
     }
-    nlp->g(nlp->ctx, w, C.gv);
+    P.obj_scale = oc.obj_scale;
+
+    ipm S;
+    ipm_alloc(&S, &P, &opts);
+    int iter = 0;
+    S.iter = &iter;
+    ora_ipm_result diag;
+    memset(&diag, 0, sizeof diag);
+    S.diag = &diag;
+
+    /* ---- starting point: x0 pushed inside (bound_push/bound_frac 0.01) ---- */
+    for (int i = 0; i < n; ++i) S.w[i] = nlp->x0[i];
+    nlp->g(nlp->ctx, S.w, oc.gv);
     for (int r = 0; r < m; ++r) {
-        int s = C.ineq_of_row[r];
-        if (s >= 0) w[n + s] = C.gv[r];
+        int s = oc.ineq_of_row[r];
+        if (s >= 0) S.w[n + s] = oc.gv[r];
     }
     for (int i = 0; i < nw; ++i) {
         const double k1 = 0.01, k2 = 0.01;
-        if (C.hasL[i] && C.hasU[i]) {
-            double pl = fmin(k1 * fmax(1.0, fabs(C.wl[i])), k2 * (C.wu[i] - C.wl[i]));
-            double pu = fmin(k1 * fmax(1.0, fabs(C.wu[i])), k2 * (C.wu[i] - C.wl[i]));
-            if (w[i] < C.wl[i] + pl) w[i] = C.wl[i] + pl;
-            if (w[i] > C.wu[i] - pu) w[i] = C.wu[i] - pu;
-        } else if (C.hasL[i]) {
-            double pl = k1 * fmax(1.0, fabs(C.wl[i]));
-            if (w[i] < C.wl[i] + pl) w[i] = C.wl[i] + pl;
-        } else if (C.hasU[i]) {
-            double pu = k1 * fmax(1.0, fabs(C.wu[i]));
-            if (w[i] > C.wu[i] - pu) w[i] = C.wu[i] - pu;
+        if (P.hasL[i] && P.hasU[i]) {
+            double pl = fmin(k1 * fmax(1.0, fabs(wl[i])), k2 * (wu[i] - wl[i]));
+            double pu = fmin(k1 * fmax(1.0, fabs(wu[i])), k2 * (wu[i] - wl[i]));
+            if (S.w[i] < wl[i] + pl) S.w[i] = wl[i] + pl;
+            if (S.w[i] > wu[i] - pu) S.w[i] = wu[i] - pu;
+        } else if (P.hasL[i]) {
+            double pl = k1 * fmax(1.0, fabs(wl[i]));
+            if (S.w[i] < wl[i] + pl) S.w[i] = wl[i] + pl;
+        } else if (P.hasU[i]) {
+            double pu = k1 * fmax(1.0, fabs(wu[i]));
+            if (S.w[i] > wu[i] - pu) S.w[i] = wu[i] - pu;
         }
     }
     for (int i = 0; i < nw; ++i) {
-        zL[i] = C.hasL[i] ? 1.0 : 0.0;
-        zU[i] = C.hasU[i] ? 1.0 : 0.0;
+        S.zL[i] = P.hasL[i] ? 1.0 : 0.0;
+        S.zU[i] = P.hasU[i] ? 1.0 : 0.0;
     }
-    int nbnd = 0;
-    for (int i = 0; i < nw; ++i) nbnd += C.hasL[i] + C.hasU[i];
-
     /* ---- least-squares multiplier estimate (constr_mult_init_max 1000) ---- */
-    eval_grad(&C, w, gf);
-    eval_A(&C, w, A);
-    memset(KKT, 0, sizeof(double) * (size_t)K * K);
-    for (int i = 0; i < nw; ++i) KKT[i + (size_t)i * K] = 1.0;
-    for (int r = 0; r < m; ++r)
-        for (int j = 0; j < nw; ++j) KKT[(nw + r) + (size_t)j * K] = A[(size_t)r * nw + j];
-    for (int i = 0; i < nw; ++i) rhs[i] = -(gf[i] - zL[i] + zU[i]);
-    for (int r = 0; r < m; ++r) rhs[nw + r] = 0.0;
     {
-        int np, nn, nz;
-        ora_ldlt_factor(K, KKT, ipiv, 1e-300, &np, &nn, &nz);
-        if (nz == 0) {
-            ora_ldlt_solve(K, KKT, ipiv, rhs);
-            double ym = amax(m, rhs + nw);
-            for (int r = 0; r < m; ++r) y[r] = (ym <= 1000.0) ? rhs[nw + r] : 0.0;
-        } else {
-            for (int r = 0; r < m; ++r) y[r] = 0.0;
-        }
-    }
-
-    double mu = opts.mu_init;
-    const double mu_min = opts.tol / 10.0;
-    double tau = fmax(0.99, 1.0 - mu);
-    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, kappa_sigma = 1e10;
-    const double gamma_theta = 1e-5, gamma_phi = 1e-8, delta_sw = 1.0, gamma_alpha = 0.05;
-    const double s_theta = 1.1, s_phi = 2.3, eta_phi = 1e-8;
-    eval_c(&C, w, cv);
-    const double theta0 = l1(m, cv);
-    const double theta_max = 1e4 * fmax(1.0, theta0);
-    const double theta_min = 1e-4 * fmax(1.0, theta0);
-    double delta_w_last = 0.0;
-    int status = ORA_MAXITER_EXCEEDED;
-    int iter = 0;
-    double final_err = INFINITY;
-
-    for (iter = 0; iter <= opts.max_iter; ++iter) {
-        /* ---- evaluate at current iterate ---- */
-        eval_grad(&C, w, gf);
-        eval_c(&C, w, cv);
-        eval_A(&C, w, A);
-        for (int i = 0; i < nw; ++i) rd[i] = gf[i] - zL[i] + zU[i];
+        const int K = S.K;
+        P.grad(&P, S.w, 0.0, S.gf);
+        P.jac(&P, S.w, S.A);
+        memset(S.KKT, 0, sizeof(double) * (size_t)K * K);
+        for (int i = 0; i < nw; ++i) S.KKT[i + (size_t)i * K] = 1.0;
         for (int r = 0; r < m; ++r)
-            for (int j = 0; j < nw; ++j) rd[j] += A[(size_t)r * nw + j] * y[r];
-        double sd = fmax(100.0, (l1(m, y) + l1(nw, zL) + l1(nw, zU)) / (double)(m + nbnd > 0 ? m + nbnd : 1)) / 100.0;
-        double sc = fmax(100.0, (l1(nw, zL) + l1(nw, zU)) / (double)(nbnd > 0 ? nbnd : 1)) / 100.0;
-        double dual_inf = amax(nw, rd);
-        double prim_inf = amax(m, cv);
-        double compl0 = 0.0;
-        for (int i = 0; i < nw; ++i) {
-            if (C.hasL[i]) compl0 = fmax(compl0, fabs((w[i] - C.wl[i]) * zL[i]));
-            if (C.hasU[i]) compl0 = fmax(compl0, fabs((C.wu[i] - w[i]) * zU[i]));
-        }
-        double E0 = fmax(dual_inf / sd, fmax(prim_inf, compl0 / sc));
-        /* unscaled checks (Ipopt dual_inf_tol / constr_viol_tol / compl_inf_tol) */
-        double dual_unscaled = dual_inf / C.obj_scale;
-        double prim_unscaled = 0.0;
-        for (int r = 0; r < m; ++r) prim_unscaled = fmax(prim_unscaled, fabs(cv[r] / C.c_scale[r]));
-        final_err = fmax(dual_unscaled, fmax(prim_unscaled, compl0));
-        if (opts.print_level > 0)
-            fprintf(stderr, "iter %3d mu %.2e E0 %.3e dual %.3e prim %.3e compl %.3e f %.10e\n", iter,
-                    mu, E0, dual_inf, prim_inf, compl0, eval_f(&C, w) / C.obj_scale);
-        /* Ipopt's finiteness test of f and g at an evaluated point (OrigIpoptNLP, Ipopt
-         * 3.12.8, not vendored in the reference) -> INVALID_NUMBER_DETECTED: amax()
-         * drops a NaN, the l1 norm and f do not */
-        if (!isfinite(E0) || !isfinite(l1(m, cv)) || !isfinite(eval_f(&C, w))) {
-            status = ORA_INVALID_NUMBER_DETECTED;
-            break;
-        }
-        if (E0 <= opts.tol && dual_unscaled <= 1.0 && prim_unscaled <= 1e-4 && compl0 <= 1e-4) {
-            status = ORA_SUCCESS;
-            break;
-        }
-        if (iter == opts.max_iter) { status = ORA_MAXITER_EXCEEDED; break; }
-
-        /* ---- monotone barrier update (A-3), possibly several times ---- */
-        for (;;) {
-            double complmu = 0.0;
-            for (int i = 0; i < nw; ++i) {
-                if (C.hasL[i]) complmu = fmax(complmu, fabs((w[i] - C.wl[i]) * zL[i] - mu));
-                if (C.hasU[i]) complmu = fmax(complmu, fabs((C.wu[i] - w[i]) * zU[i] - mu));
-            }
-            double Emu = fmax(dual_inf / sd, fmax(prim_inf, complmu / sc));
-            if (Emu > kappa_eps * mu || mu <= mu_min) break;
-            double mnew = fmax(mu_min, fmin(kappa_mu * mu, pow(mu, theta_mu)));
-            if (mnew >= mu) break;
-            mu = mnew;
-            tau = fmax(0.99, 1.0 - mu);
-            nfilter = 0;
-        }
-
-        /* ---- primal-dual system with inertia correction (Algorithm IC) ---- */
-        eval_W(&C, w, y, W);
-        barrier_grad(&C, w, mu, gf, gphi);
-        double delta_w = 0.0, delta_c = 0.0;
-        int attempt = 0, ok = 0;
-        for (;;) {
-            memset(KKT, 0, sizeof(double) * (size_t)K * K);
-            for (int j = 0; j < n; ++j)
-                for (int i = j; i < n; ++i) KKT[i + (size_t)j * K] = W[(size_t)i * n + j];
-            for (int i = 0; i < nw; ++i) {
-                double sig = 0.0;
-                if (C.hasL[i]) sig += zL[i] / (w[i] - C.wl[i]);
-                if (C.hasU[i]) sig += zU[i] / (C.wu[i] - w[i]);
-                KKT[i + (size_t)i * K] += sig + delta_w;
-            }
-            for (int r = 0; r < m; ++r) {
-                for (int j = 0; j < nw; ++j) KKT[(nw + r) + (size_t)j * K] = A[(size_t)r * nw + j];
-                KKT[(nw + r) + (size_t)(nw + r) * K] = -delta_c;
-            }
-            int np, nn, nz;
-            ora_ldlt_factor(K, KKT, ipiv, 1e-300, &np, &nn, &nz);
-            if (np == nw && nn == m && nz == 0) {
-                ok = 1;
-                if (delta_w > 0) delta_w_last = delta_w;
-                break;
-            }
-            if (nz > 0 && delta_c == 0.0) delta_c = 1e-8 * pow(mu, 0.25);
-            if (attempt == 0) {
-                delta_w = (delta_w_last == 0.0) ? 1e-4 : fmax(1e-20, delta_w_last / 3.0);
-            } else {
-                delta_w = (delta_w_last == 0.0) ? 100.0 * delta_w : 8.0 * delta_w;
-            }
-            ++attempt;
-            if (delta_w > 1e40) break;
-        }
-        if (!ok) { status = ORA_ERROR_IN_STEP_COMPUTATION; break; }
-        for (int i = 0; i < nw; ++i) {
-            double s = gphi[i];
-            for (int r = 0; r < m; ++r) s += A[(size_t)r * nw + i] * y[r];
-            rhs[i] = -s;
-        }
-        for (int r = 0; r < m; ++r) rhs[nw + r] = -cv[r];
-        ora_ldlt_solve(K, KKT, ipiv, rhs);
-        for (int i = 0; i < nw; ++i) dw[i] = rhs[i];
-        for (int r = 0; r < m; ++r) dy[r] = rhs[nw + r];
-        for (int i = 0; i < nw; ++i) {
-            dzL[i] = C.hasL[i] ? mu / (w[i] - C.wl[i]) - zL[i] - zL[i] / (w[i] - C.wl[i]) * dw[i] : 0.0;
-            dzU[i] = C.hasU[i] ? mu / (C.wu[i] - w[i]) - zU[i] + zU[i] / (C.wu[i] - w[i]) * dw[i] : 0.0;
-        }
-
-        /* ---- fraction-to-the-boundary ---- */
-        double amax_p = 1.0, amax_z = 1.0;
-        for (int i = 0; i < nw; ++i) {
-            if (C.hasL[i] && dw[i] < 0) amax_p = fmin(amax_p, -tau * (w[i] - C.wl[i]) / dw[i]);
-            if (C.hasU[i] && dw[i] > 0) amax_p = fmin(amax_p, tau * (C.wu[i] - w[i]) / dw[i]);
-            if (C.hasL[i] && dzL[i] < 0) amax_z = fmin(amax_z, -tau * zL[i] / dzL[i]);
-            if (C.hasU[i] && dzU[i] < 0) amax_z = fmin(amax_z, -tau * zU[i] / dzU[i]);
-        }
-
-        /* ---- filter line search (A-5) ---- */
-        int okphi;
-        double phik = barrier_phi(&C, w, mu, &okphi);
-        double thetak = l1(m, cv);
-        double gd = 0.0;
-        for (int i = 0; i < nw; ++i) gd += gphi[i] * dw[i];
-        double alpha_min;
-        if (gd < 0 && thetak <= theta_min)
-            alpha_min = gamma_alpha * fmin(gamma_theta, fmin(-gamma_phi * thetak / gd,
-                                                             delta_sw * pow(thetak, s_theta) / pow(-gd, s_phi)));
-        else if (gd < 0)
-            alpha_min = gamma_alpha * fmin(gamma_theta, -gamma_phi * thetak / gd);
-        else
-            alpha_min = gamma_alpha * gamma_theta;
-        /* tiny step (Ipopt's tiny_step_tol = 10*eps_mach) */
-        double rel = 0.0;
-        for (int i = 0; i < nw; ++i) rel = fmax(rel, fabs(dw[i]) / (1.0 + fabs(w[i])));
-        int tiny = (rel < 10.0 * 2.2e-16);
-        double alpha = amax_p;
-        int accepted = 0, ftype = 0;
-        for (int ls = 0; ls < 60; ++ls) {
-            for (int i = 0; i < nw; ++i) wt[i] = w[i] + alpha * dw[i];
-            if (tiny) { accepted = 1; ftype = 1; break; }
-            if (alpha < alpha_min) break;
-            int okt;
-            double phit = barrier_phi(&C, wt, mu, &okt);
-            eval_c(&C, wt, ct);
-            double thetat = l1(m, ct);
-            if (okt && isfinite(thetat) && thetat < theta_max) {
-                int infilt = 0;
-                for (int f = 0; f < nfilter; ++f)
-                    if (thetat >= filter[f].th && phit >= filter[f].ph) { infilt = 1; break; }
-                if (!infilt) {
-                    int sw = (gd < 0) && (alpha * pow(-gd, s_phi) > delta_sw * pow(thetak, s_theta));
-                    if (thetak <= theta_min && sw) {
-                        if (phit <= phik + eta_phi * alpha * gd) { accepted = 1; ftype = 1; break; }
-                    } else if (thetat <= (1.0 - gamma_theta) * thetak || phit <= phik - gamma_phi * thetak) {
-                        accepted = 1;
-                        ftype = 0;
-                        break;
-                    }
-                }
-            }
-            alpha *= 0.5;
-        }
-        if (!accepted) { status = ORA_RESTORATION_FAILURE; break; }
-        if (!ftype) {
-            if (nfilter == capfilter) {
-                capfilter *= 2;
-                filter = (fpair*)realloc(filter, sizeof(fpair) * capfilter);
-            }
-            filter[nfilter].th = (1.0 - gamma_theta) * thetak;
-            filter[nfilter].ph = phik - gamma_phi * thetak;
-            ++nfilter;
-        }
-        /* ---- accept ---- */
-        for (int i = 0; i < nw; ++i) w[i] = wt[i];
-        for (int r = 0; r < m; ++r) y[r] += alpha * dy[r];
-        for (int i = 0; i < nw; ++i) {
-            if (C.hasL[i]) {
-                double z = zL[i] + amax_z * dzL[i];
-                double s = w[i] - C.wl[i];
-                zL[i] = fmax(fmin(z, kappa_sigma * mu / s), mu / (kappa_sigma * s));
-            }
-            if (C.hasU[i]) {
-                double z = zU[i] + amax_z * dzU[i];
-                double s = C.wu[i] - w[i];
-                zU[i] = fmax(fmin(z, kappa_sigma * mu / s), mu / (kappa_sigma * s));
-            }
+            for (int j = 0; j < nw; ++j) S.KKT[(nw + r) + (size_t)j * K] = S.A[(size_t)r * nw + j];
+        for (int i = 0; i < nw; ++i) S.rhs[i] = -(S.gf[i] - S.zL[i] + S.zU[i]);
+        for (int r = 0; r < m; ++r) S.rhs[nw + r] = 0.0;
+        int np, nn, nz;
+        ora_ldlt_factor(K, S.KKT, S.ipiv, 1e-300, &np, &nn, &nz);
+        if (nz == 0) {
+            ora_ldlt_solve(K, S.KKT, S.ipiv, S.rhs);
+            double ym = amax(m, S.rhs + nw);
+            for (int r = 0; r < m; ++r) S.y[r] = (ym <= 1000.0) ? S.rhs[nw + r] : 0.0;
         }
     }
+    S.mu = opts.mu_init;
+    S.tau = fmax(0.99, 1.0 - S.mu);
+
+    int status = ipm_iterate(&S);
 
     /* ---- outputs (unscaled), honor_original_bounds ---- */
     for (int i = 0; i < n; ++i) {
-        double xv = w[i];
+        double xv = S.w[i];
         if (opts.honor_original_bounds) {
-            if (C.hasL[i] && xv < wl0[i]) xv = wl0[i];
-            if (C.hasU[i] && xv > wu0[i]) xv = wu0[i];
+            if (P.hasL[i] && xv < wl0[i]) xv = wl0[i];
+            if (P.hasU[i] && xv > wu0[i]) xv = wu0[i];
         }
         x_out[i] = xv;
-        if (zl_out) zl_out[i] = zL[i] / C.obj_scale;
-        if (zu_out) zu_out[i] = zU[i] / C.obj_scale;
+        if (zl_out) zl_out[i] = S.zL[i] / oc.obj_scale;
+        if (zu_out) zu_out[i] = S.zU[i] / oc.obj_scale;
     }
     if (lambda_out)
-        for (int r = 0; r < m; ++r) lambda_out[r] = y[r] * C.c_scale[r] / C.obj_scale;
+        for (int r = 0; r < m; ++r) lambda_out[r] = S.y[r] * oc.c_scale[r] / oc.obj_scale;
     if (g_out) nlp->g(nlp->ctx, x_out, g_out);
     if (res) {
+        *res = diag;
         res->status = status;
         res->iters = iter;
         res->obj = nlp->f(nlp->ctx, x_out);
-        res->kkt_inf = final_err;
+        res->kkt_inf = fmax(S.dual_uns, fmax(S.prim_uns, S.compl_uns));
     }
-    free(ipiv);
-    free(C.hasL);
-    free(C.hasU);
-    free(C.ineq_of_row);
-    free(filter);
-    free(mem);
+    ipm_free(&S);
+    free(oc.ineq_of_row);
+    free(buf);
+    free(hb);
     return status;
 }

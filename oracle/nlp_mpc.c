@@ -256,8 +256,8 @@ static void cb_hess(void* ctx, const double* x, double sigma, const double* lam,
     ora_mpc_hess(m->p, m->c, x, sigma, lam, H);
 }
 
-int ora_mpc_solve(const ora_mpc_params* p, const ora_ipm_opts* opts, const double* st, const double* coeffs,
-                  double* u0, double* traj, double* obj, int* iters, double* kkt_inf, double* xfull) {
+int ora_mpc_solve_res(const ora_mpc_params* p, const ora_ipm_opts* opts, const double* st, const double* coeffs,
+                      double* u0, double* traj, double* xfull, ora_ipm_result* res) {
     const int N = p->steps;
     const int nx = ora_mpc_nx(N), ng = ora_mpc_ng(N);
     double* buf = (double*)malloc(sizeof(double) * (size_t)(6 * nx + 3 * ng + 1));
@@ -280,8 +280,7 @@ int ora_mpc_solve(const ora_mpc_params* p, const ora_ipm_opts* opts, const doubl
     nlp.gu = gu;
     nlp.x0 = x0;
     double* lam = (double*)malloc(sizeof(double) * (size_t)ng * 2);
-    ora_ipm_result res;
-    int status = ora_ipm_solve(&nlp, opts, x, zl, zu, lam, lam + ng, &res);
+    int status = ora_ipm_solve(&nlp, opts, x, zl, zu, lam, lam + ng, res);
     /* outputs, mpc_planner.cpp:388-401 */
     for (int i = 0; i < N; ++i) {
         traj[i] = x[IX(N) + i];
@@ -290,18 +289,25 @@ int ora_mpc_solve(const ora_mpc_params* p, const ora_ipm_opts* opts, const doubl
     }
     u0[0] = x[IW(N)];
     u0[1] = x[IA(N)];
-    if (obj) *obj = res.obj;
-    if (iters) *iters = res.iters;
-    if (kkt_inf) *kkt_inf = res.kkt_inf;
     if (xfull) memcpy(xfull, x, sizeof(double) * nx);
     free(lam);
     free(buf);
     return status;
 }
 
-int ora_mpc_solve_batch(const ora_mpc_params* p, const ora_ipm_opts* opts, int64_t B, const double* state,
-                        const double* coeffs, double* u0, double* traj, double* obj, int32_t* status,
-                        int32_t* iters, int nthreads) {
+int ora_mpc_solve(const ora_mpc_params* p, const ora_ipm_opts* opts, const double* st, const double* coeffs,
+                  double* u0, double* traj, double* obj, int* iters, double* kkt_inf, double* xfull) {
+    ora_ipm_result res;
+    int status = ora_mpc_solve_res(p, opts, st, coeffs, u0, traj, xfull, &res);
+    if (obj) *obj = res.obj;
+    if (iters) *iters = res.iters;
+    if (kkt_inf) *kkt_inf = res.kkt_inf;
+    return status;
+}
+
+int ora_mpc_solve_batch_diag(const ora_mpc_params* p, const ora_ipm_opts* opts, int64_t B, const double* state,
+                             const double* coeffs, double* u0, double* traj, double* obj, int32_t* status,
+                             int32_t* iters, int32_t* diag, int nthreads) {
     const int N = p->steps;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -310,15 +316,28 @@ int ora_mpc_solve_batch(const ora_mpc_params* p, const ora_ipm_opts* opts, int64
     (void)nthreads;
 #endif
     for (int64_t b = 0; b < B; ++b) {
-        double ob, kk;
-        int it;
-        int st = ora_mpc_solve(p, opts, state + 6 * b, coeffs + 4 * b, u0 + 2 * b, traj + (size_t)3 * N * b, &ob,
-                               &it, &kk, NULL);
-        if (obj) obj[b] = ob;
+        ora_ipm_result res;
+        int st = ora_mpc_solve_res(p, opts, state + 6 * b, coeffs + 4 * b, u0 + 2 * b, traj + (size_t)3 * N * b,
+                                   NULL, &res);
+        if (obj) obj[b] = res.obj;
         if (status) status[b] = st;
-        if (iters) iters[b] = it;
+        if (iters) iters[b] = res.iters;
+        if (diag) {
+            int32_t* d = diag + 5 * b;
+            d[0] = res.n_soc;
+            d[1] = res.n_watchdog;
+            d[2] = res.n_soft_resto;
+            d[3] = res.n_resto;
+            d[4] = res.resto_iters;
+        }
     }
     return 0;
+}
+
+int ora_mpc_solve_batch(const ora_mpc_params* p, const ora_ipm_opts* opts, int64_t B, const double* state,
+                        const double* coeffs, double* u0, double* traj, double* obj, int32_t* status,
+                        int32_t* iters, int nthreads) {
+    return ora_mpc_solve_batch_diag(p, opts, B, state, coeffs, u0, traj, obj, status, iters, NULL, nthreads);
 }
 
 /* Independent first-order certificate for a primal point x of the NLP: the

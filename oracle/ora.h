@@ -62,6 +62,29 @@ typedef struct ora_ipm_opts {
     int honor_original_bounds;  /* default 1 */
     double mu_init;             /* default 0.1 */
     int print_level;            /* 0 = silent */
+    /* ---- Ipopt 3.12 defaults restated in round 2 (0 / negative disables a feature) ---- */
+    double acceptable_tol;              /* 1e-6 */
+    int acceptable_iter;                /* 15 (0: no acceptable termination) */
+    double acceptable_dual_inf_tol;     /* 1e10 */
+    double acceptable_constr_viol_tol;  /* 1e-2 */
+    double acceptable_compl_inf_tol;    /* 1e-2 */
+    double acceptable_obj_change_tol;   /* 1e20 */
+    int max_soc;                        /* 4 (second-order corrections) */
+    double kappa_soc;                   /* 0.99 */
+    int watchdog_shortened_iter_trigger;/* 10 (0: no watchdog) */
+    int watchdog_trial_iter_max;        /* 3 */
+    double soft_resto_pderror_reduction_factor; /* 0.9999 (0: no soft restoration) */
+    int max_soft_resto_iters;           /* 10 */
+    int restoration;                    /* 1: feasibility restoration phase; 0: RESTORATION_FAILURE */
+    double obj_max_inc;                 /* 5 */
+    int max_filter_resets;              /* 5 */
+    int filter_reset_trigger;           /* 5 */
+    double tiny_step_tol;               /* 10 eps */
+    double tiny_step_y_tol;             /* 1e-2 */
+    /* the reference's "max_cpu_time 0.5" (mpc_planner.cpp:368) as a deterministic iteration
+     * budget: CPUTIME_EXCEEDED (-> solve_result unknown, solve_callback.hpp:1165-1167) once
+     * iter > cpu_iter_budget; < 0 = no budget (see ora_cpu_iter_budget) */
+    int cpu_iter_budget;
 } ora_ipm_opts;
 
 /* Result; status uses CppAD::ipopt::solve_result::status_type numbering
@@ -79,10 +102,19 @@ typedef struct ora_ipm_result {
     int iters;
     double obj;
     double kkt_inf;             /* final unscaled max(dual inf, primal inf, compl) */
+    /* diagnostics: second-order corrections accepted, watchdog activations, soft
+     * restoration steps, restoration phases entered, restoration-phase iterations */
+    int n_soc, n_watchdog, n_soft_resto, n_resto, resto_iters;
     /* x[n], zl[n], zu[n], lambda[m], g[m] written to caller buffers */
 } ora_ipm_result;
 
 void ora_ipm_default_opts(ora_ipm_opts* o);
+/* Iteration budget equivalent to max_cpu_time seconds of the reference's Solve at horizon
+ * N: (max_cpu_time - setup(N)) / per_iter(N), with the CppAD taping and per-iteration
+ * derivative costs measured in this container (1.52 ms + 0.225 ms/iter at
+ * N = 20, 3.93 ms + 0.467 ms/iter at N = 40, linear in N).  Ipopt's own linear algebra
+ * is not included (Ipopt is absent), so the budget errs generous. */
+int ora_cpu_iter_budget(double max_cpu_time, int steps);
 int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts, double* x, double* zl,
                   double* zu, double* lambda, double* gval, ora_ipm_result* res);
 
@@ -121,6 +153,15 @@ void ora_mpc_bounds(const ora_mpc_params* p, const double* state6, double* x0, d
 int ora_mpc_solve(const ora_mpc_params* p, const ora_ipm_opts* opts, const double* state6,
                   const double* coeffs4, double* u0, double* traj, double* obj, int* iters,
                   double* kkt_inf, double* xfull);
+
+/* ora_mpc_solve with the solver's diagnostics (ora_ipm_result) */
+int ora_mpc_solve_res(const ora_mpc_params* p, const ora_ipm_opts* opts, const double* state6,
+                      const double* coeffs4, double* u0, double* traj, double* xfull, ora_ipm_result* res);
+/* Batched, with per-problem diagnostics diag[B][5] = n_soc, n_watchdog, n_soft_resto,
+ * n_resto, resto_iters (may be NULL). */
+int ora_mpc_solve_batch_diag(const ora_mpc_params* p, const ora_ipm_opts* opts, int64_t B,
+                             const double* state, const double* coeffs, double* u0, double* traj,
+                             double* obj, int32_t* status, int32_t* iters, int32_t* diag, int nthreads);
 
 /* Batched convenience (OpenMP over problems when built with -fopenmp). */
 int ora_mpc_solve_batch(const ora_mpc_params* p, const ora_ipm_opts* opts, int64_t B,

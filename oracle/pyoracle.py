@@ -30,6 +30,14 @@ class IpmOpts(C.Structure):
     _fields_ = [
         ("tol", C.c_double), ("max_iter", C.c_int), ("bound_relax_factor", C.c_double),
         ("honor_original_bounds", C.c_int), ("mu_init", C.c_double), ("print_level", C.c_int),
+        ("acceptable_tol", C.c_double), ("acceptable_iter", C.c_int), ("acceptable_dual_inf_tol", C.c_double),
+        ("acceptable_constr_viol_tol", C.c_double), ("acceptable_compl_inf_tol", C.c_double),
+        ("acceptable_obj_change_tol", C.c_double), ("max_soc", C.c_int), ("kappa_soc", C.c_double),
+        ("watchdog_shortened_iter_trigger", C.c_int), ("watchdog_trial_iter_max", C.c_int),
+        ("soft_resto_pderror_reduction_factor", C.c_double), ("max_soft_resto_iters", C.c_int),
+        ("restoration", C.c_int), ("obj_max_inc", C.c_double), ("max_filter_resets", C.c_int),
+        ("filter_reset_trigger", C.c_int), ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
+        ("cpu_iter_budget", C.c_int),
     ]
 
 
@@ -60,6 +68,10 @@ def lib():
         L.ora_mpc_hess.argtypes = [C.POINTER(MpcParams), dp, dp, C.c_double, dp, dp]
         L.ora_mpc_bounds.argtypes = [C.POINTER(MpcParams), dp, dp, dp, dp, dp, dp]
         L.ora_mpc_solve.argtypes = [C.POINTER(MpcParams), C.POINTER(IpmOpts), dp, dp, dp, dp, dp, ip, dp, dp]
+        L.ora_mpc_solve_batch_diag.argtypes = [C.POINTER(MpcParams), C.POINTER(IpmOpts), C.c_int64, dp, dp, dp, dp,
+                                               dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_int32), C.c_int]
+        L.ora_cpu_iter_budget.argtypes = [C.c_double, C.c_int]
         L.ora_mpc_solve_batch.argtypes = [C.POINTER(MpcParams), C.POINTER(IpmOpts), C.c_int64, dp, dp, dp, dp,
                                           dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
         L.ora_mpc_kkt_residual.argtypes = [C.POINTER(MpcParams), dp, dp, dp, dp, dp, dp]
@@ -99,7 +111,9 @@ def params_from_dict(d: dict) -> MpcParams:
 
 
 def ipm_opts(tol: float = 1e-10, max_iter: int = 3000, bound_relax_factor: float = 1e-8,
-             honor_original_bounds: int = 1, print_level: int = 0) -> IpmOpts:
+             honor_original_bounds: int = 1, print_level: int = 0, **kw) -> IpmOpts:
+    """Ipopt 3.12 defaults (oracle/ipm.c ora_ipm_default_opts) with the given overrides;
+    keyword arguments are further IpmOpts fields (e.g. max_soc=0, cpu_iter_budget=40)."""
     o = IpmOpts()
     lib().ora_ipm_default_opts(C.byref(o))
     o.tol = tol
@@ -107,7 +121,23 @@ def ipm_opts(tol: float = 1e-10, max_iter: int = 3000, bound_relax_factor: float
     o.bound_relax_factor = bound_relax_factor
     o.honor_original_bounds = honor_original_bounds
     o.print_level = print_level
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise AttributeError(k)
+        setattr(o, k, v)
     return o
+
+
+def ref_opts(steps: int, **kw) -> IpmOpts:
+    """The reference's solver options (mpc_planner.cpp:356-368): Ipopt 3.12 defaults with
+    max_cpu_time 0.5 s applied as its iteration budget at this horizon."""
+    kw.setdefault("cpu_iter_budget", cpu_iter_budget(0.5, steps))
+    return ipm_opts(tol=1e-8, **kw)
+
+
+def cpu_iter_budget(max_cpu_time: float, steps: int) -> int:
+    """Iterations equivalent to max_cpu_time seconds of the reference's Solve (ora.h)."""
+    return int(lib().ora_cpu_iter_budget(float(max_cpu_time), int(steps)))
 
 
 def mpc_solve(params: dict, state, coeffs, opts: IpmOpts | None = None, full: bool = False):
@@ -132,7 +162,7 @@ def mpc_solve(params: dict, state, coeffs, opts: IpmOpts | None = None, full: bo
 
 
 def mpc_solve_batch(params: dict, state: np.ndarray, coeffs: np.ndarray, opts: IpmOpts | None = None,
-                    nthreads: int = 0):
+                    nthreads: int = 0, diag: bool = False):
     L = lib()
     p = params_from_dict(params)
     o = opts or ipm_opts()
@@ -145,10 +175,14 @@ def mpc_solve_batch(params: dict, state: np.ndarray, coeffs: np.ndarray, opts: I
     obj = np.zeros(B)
     status = np.zeros(B, dtype=np.int32)
     iters = np.zeros(B, dtype=np.int32)
-    L.ora_mpc_solve_batch(C.byref(p), C.byref(o), B, _dp(st), _dp(cf), _dp(u0), _dp(traj), _dp(obj),
-                          status.ctypes.data_as(C.POINTER(C.c_int32)), iters.ctypes.data_as(C.POINTER(C.c_int32)),
-                          int(nthreads))
-    return dict(u0=u0, traj=traj, obj=obj, status=status, iters=iters)
+    dg = np.zeros((B, 5), dtype=np.int32)
+    L.ora_mpc_solve_batch_diag(C.byref(p), C.byref(o), B, _dp(st), _dp(cf), _dp(u0), _dp(traj), _dp(obj),
+                               status.ctypes.data_as(C.POINTER(C.c_int32)), iters.ctypes.data_as(C.POINTER(C.c_int32)),
+                               dg.ctypes.data_as(C.POINTER(C.c_int32)), int(nthreads))
+    out = dict(u0=u0, traj=traj, obj=obj, status=status, iters=iters)
+    if diag:  # per problem: n_soc, n_watchdog, n_soft_resto, n_resto, resto_iters
+        out["diag"] = dg
+    return out
 
 
 def mpc_fg(params: dict, coeffs, vars_):

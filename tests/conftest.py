@@ -66,6 +66,24 @@ def bicycle_golden():
 
 
 @pytest.fixture(scope="session")
+def features_golden():
+    """tests/golden/ipopt_features.npz split by set (N20, N40, bicycle, budget); each set
+    carries its parameter dict as "P"."""
+    z = load_npz("ipopt_features.npz")
+    out = {}
+    for k, v in z.items():
+        if "__" in k:
+            name, field = k.split("__", 1)
+            out.setdefault(name, {})[field] = v
+    for name, g in out.items():
+        P = params_from_array(g["params"])
+        if name == "bicycle":
+            P.update(MODEL=1, LF=0.5)
+        g["P"] = P
+    return out
+
+
+@pytest.fixture(scope="session")
 def libmpcg():
     from mpc_ros_amd import build, _lib
 

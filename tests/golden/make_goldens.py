@@ -17,6 +17,15 @@ Fixtures (data only -- inputs and expected outputs):
   bicycle_N25.npz    the kinematic-bicycle variant (BASELINE configs[4]; no reference
                      implementation exists, so this pins the build's own restatement):
                      64 infinity-set problems, N = 25, MODEL = 1, LF = 0.5, ANGVEL = 0.5
+  ipopt_features.npz problems of the infinity set on which Ipopt's second-order
+                     corrections, watchdog, soft restoration and restoration phase act
+                     (found by scanning with the oracle's diagnostics), the problems the
+                     round-1 advisor named for the bounded filter (16101, 1887), and the
+                     max_cpu_time iteration budget forced low; per problem the parameter
+                     set (N20 / N40 / bicycle), the oracle's diagnostics and results
+
+All solves use the reference's options (oracle.pyoracle.ref_opts: Ipopt 3.12 defaults,
+max_cpu_time 0.5 s as its iteration budget).
 
     python tests/golden/make_goldens.py [set ...]     (default: all sets)
 """
@@ -75,10 +84,11 @@ def cppad_derivs():
     np.savez_compressed(os.path.join(HERE, "cppad_derivs.npz"), **out)
 
 
-def solve_set(P, st, cf):
-    r = O.mpc_solve_batch(P, st, cf, opts=O.ipm_opts(tol=1e-8), nthreads=os.cpu_count() or 8)
+def solve_set(P, st, cf, opts=None):
+    r = O.mpc_solve_batch(P, st, cf, opts=opts or O.ref_opts(int(P["STEPS"])), nthreads=os.cpu_count() or 8,
+                          diag=True)
     return dict(state=st, coeffs=cf, u0=r["u0"], traj=r["traj"], obj=r["obj"], status=r["status"],
-                iters=r["iters"], params=np.array([P[k] for k in params.KEYS]))
+                iters=r["iters"], diag=r["diag"], params=np.array([P[k] for k in params.KEYS]))
 
 
 def infinity_set():
@@ -141,6 +151,44 @@ def bicycle():
     print("bicycle_N25 status:", np.unique(d["status"], return_counts=True), "iters mean", d["iters"].mean())
 
 
+FEATURE_SETS = {
+    # name: (params, problem indices of the infinity set)
+    # N20: second-order corrections (7, 11, 25, 932: different local minimum without them;
+    # 2571: two corrections), soft restoration (5045, 8938), restoration phase (1443),
+    # round-1 advisor's filter-size problems (1887, 16101)
+    "N20": (PLUGIN, [7, 11, 25, 932, 2571, 5045, 8938, 1443, 1887, 16101]),
+    # N40: watchdog (88: six activations, 460, 842, 2012, 2094), soft restoration (422, 429,
+    # 1431), restoration phase (69, 1167, 1204, 2956, 3441)
+    "N40": (dict(PLUGIN, STEPS=40), [88, 460, 842, 2012, 2094, 422, 429, 1431, 69, 1167, 1204, 2956, 3441]),
+    # bicycle N25: watchdog (3308), soft restoration (1292), corrections (18, 23)
+    "bicycle": (BICYCLE, [3308, 1292, 18, 23]),
+}
+
+
+def ipopt_features():
+    out = {}
+    for name, (P, idx) in FEATURE_SETS.items():
+        st, cf = infinity.make_problems(np.array(idx))
+        d = solve_set(P, st, cf)
+        d["index"] = np.array(idx)
+        for k, v in d.items():
+            out[f"{name}__{k}"] = v
+        print(name, "status", d["status"].tolist(), "iters", d["iters"].tolist())
+        print("   diag (soc, watchdog, soft, resto, resto iters):", d["diag"].tolist())
+    # the max_cpu_time budget forced low: 0.004 s -> ora_cpu_iter_budget iterations at N = 20
+    P = PLUGIN
+    st, cf = infinity.make_problems(np.arange(0, 32))
+    budget = O.cpu_iter_budget(0.004, 20)
+    d = solve_set(P, st, cf, opts=O.ref_opts(20, cpu_iter_budget=budget))
+    for k, v in d.items():
+        out[f"budget__{k}"] = v
+    out["budget__max_cpu_time"] = np.float64(0.004)
+    out["budget__iter_budget"] = np.int32(budget)
+    print("budget", budget, "status", np.unique(d["status"], return_counts=True))
+    out["keys"] = np.array(params.KEYS)
+    np.savez_compressed(os.path.join(HERE, "ipopt_features.npz"), **out)
+
+
 def hs071():
     with open(os.path.join(HERE, "hs071.json"), "w") as f:
         json.dump({"source": "assets/document/example/CppAD_Ipopt.cpp:146-150",
@@ -150,7 +198,7 @@ def hs071():
 
 if __name__ == "__main__":
     O.build(force=True)
-    sets = set(sys.argv[1:]) or {"hs071", "preprocess", "infinity", "variants", "bicycle", "cppad"}
+    sets = set(sys.argv[1:]) or {"hs071", "preprocess", "infinity", "variants", "bicycle", "features", "cppad"}
     if "hs071" in sets:
         hs071()
     if "preprocess" in sets:
@@ -161,6 +209,8 @@ if __name__ == "__main__":
         variants()
     if "bicycle" in sets:
         bicycle()
+    if "features" in sets:
+        ipopt_features()
     if "cppad" in sets:
         if os.path.isdir("/root/reference/mpc_ros/include/cppad"):
             cppad_derivs()

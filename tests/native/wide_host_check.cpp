@@ -4,8 +4,16 @@
 // host: the 64 lanes of a wavefront are 64 threads, LDS is a shared array, a lane
 // exchange is a store / barrier / load / barrier, and the wave barrier is a
 // std::barrier.  The butterflies run the same pairwise operations as the device
-// shuffles.  Same stdin/stdout format as ipm_host_check.cpp.  Never part of the
-// product library.
+// shuffles.  Never part of the product library.
+//
+// stdin:  N dt ref_cte ref_eth ref_v w_cte w_eth w_v w_w w_a w_dw w_da max_w max_a bound tol max_iter
+//         model lf
+//         acceptable_tol acceptable_iter acceptable_dual_inf_tol acceptable_constr_viol_tol
+//         acceptable_compl_inf_tol acceptable_obj_change_tol max_soc kappa_soc wd_trigger
+//         wd_trial_max soft_factor max_soft_iters obj_max_inc max_filter_resets
+//         filter_reset_trigger tiny_step_tol tiny_step_y_tol cpu_iter_budget filter_cap
+//         B, then B x (state[6], coeffs[4])
+// stdout: per problem: status iters obj u0[2] traj[3N]
 #include <barrier>
 #include <cmath>
 #include <cstdio>
@@ -50,6 +58,18 @@ struct HostWave {
         return r != 0;
     }
     int uni(int v) const { return v; }
+    int ballot_prefix(bool b, int* total) const {
+        sh->xi[t] = b ? 1 : 0;
+        sync();
+        int c = 0, n = 0;
+        for (int i = 0; i < 64; ++i) {
+            n += sh->xi[i];
+            if (i < t) c += sh->xi[i];
+        }
+        sync();
+        *total = n;
+        return c;
+    }
     int lane() const { return t; }
     void mark(int) const {}
     void sched_fence() const {}
@@ -113,6 +133,13 @@ int main() {
     P.model = 0;
     P.lf = 0.5;
     if (std::scanf("%d %lf", &P.model, &P.lf) != 2) return 1;
+    if (std::scanf("%lf %d %lf %lf %lf %lf %d %lf %d %d %lf %d %lf %d %d %lf %lf %d %d", &P.acceptable_tol,
+                   &P.acceptable_iter, &P.acceptable_dual_inf_tol, &P.acceptable_constr_viol_tol,
+                   &P.acceptable_compl_inf_tol, &P.acceptable_obj_change_tol, &P.max_soc, &P.kappa_soc,
+                   &P.watchdog_trigger, &P.watchdog_trial_max, &P.soft_resto_factor, &P.max_soft_resto_iters,
+                   &P.obj_max_inc, &P.max_filter_resets, &P.filter_reset_trigger, &P.tiny_step_tol,
+                   &P.tiny_step_y_tol, &P.cpu_iter_budget, &P.filter_cap) != 19)
+        return 1;
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     const mpcg::WideLayout L(P.N, P.filter_cap, P.model);
@@ -122,6 +149,7 @@ int main() {
         for (double& v : pr.c) std::scanf("%lf", &v);
         HostShared sh;
         sh.lds.assign(L.total(), std::nan(""));
+        std::vector<double> spill(L.spill(), std::nan(""));
         int status = 0, iters = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
@@ -143,16 +171,16 @@ int main() {
                     }
                 };
                 if (P.model == 1 && P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 1, true> S(P, pr, wv);
+                    mpcg::WideSolver<HostWave, 1, true> S(P, pr, wv, spill.data());
                     run(S);
                 } else if (P.model == 1) {
-                    mpcg::WideSolver<HostWave, 1, false> S(P, pr, wv);
+                    mpcg::WideSolver<HostWave, 1, false> S(P, pr, wv, spill.data());
                     run(S);
                 } else if (P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 0, true> S(P, pr, wv);
+                    mpcg::WideSolver<HostWave, 0, true> S(P, pr, wv, spill.data());
                     run(S);
                 } else {
-                    mpcg::WideSolver<HostWave, 0, false> S(P, pr, wv);
+                    mpcg::WideSolver<HostWave, 0, false> S(P, pr, wv, spill.data());
                     run(S);
                 }
             });

@@ -36,11 +36,12 @@ def test_every_declared_symbol_is_exported(libmpcg):
 def test_abi_version_and_struct_size(libmpcg):
     from mpc_ros_amd import _lib
 
-    assert libmpcg.mpcg_abi_version() == 1
+    assert libmpcg.mpcg_abi_version() == _lib.ABI_VERSION == 2
     # C struct layout: compile a tiny probe against the header and compare sizeof/offsets
-    src = ("#include <stdio.h>\n#include <stddef.h>\n#include \"mpcg.h\"\nint main(){printf(\"%zu %zu %zu %zu\","
+    src = ("#include <stdio.h>\n#include <stddef.h>\n#include \"mpcg.h\"\nint main(){printf(\"%zu %zu %zu %zu %zu %zu\","
            "sizeof(mpcg_params),offsetof(mpcg_params,tol),offsetof(mpcg_params,filter_cap),"
-           "offsetof(mpcg_params,wheelbase));}\n")
+           "offsetof(mpcg_params,wheelbase),offsetof(mpcg_params,max_cpu_time),"
+           "offsetof(mpcg_params,filter_reset_trigger));}\n")
     import tempfile
 
     with tempfile.TemporaryDirectory() as d:
@@ -49,7 +50,16 @@ def test_abi_version_and_struct_size(libmpcg):
                                os.path.join(d, "p.c")])
         got = [int(v) for v in subprocess.check_output([os.path.join(d, "p")]).split()]
     P = _lib.MpcgParams
-    assert got == [C.sizeof(P), P.tol.offset, P.filter_cap.offset, P.wheelbase.offset]
+    assert got == [C.sizeof(P), P.tol.offset, P.filter_cap.offset, P.wheelbase.offset, P.max_cpu_time.offset,
+                   P.filter_reset_trigger.offset]
+
+
+def test_build_id_is_the_source_hash(libmpcg):
+    """The library carries the hash of the sources it was built from; the loader refuses
+    a library whose id differs from the tree's sources (no stale binary on a GPU box)."""
+    from mpc_ros_amd import build
+
+    assert libmpcg.mpcg_build_id().decode() == build.source_hash() == build.built_id()
 
 
 def test_param_defaults_and_keys(libmpcg):
@@ -60,6 +70,10 @@ def test_param_defaults_and_keys(libmpcg):
     assert (p.steps, p.max_angvel, p.max_throttle, p.bound) == (20, 3.0, 1.0, 1000.0)
     assert (p.dt, p.ref_v, p.w_cte, p.w_etheta, p.w_v, p.w_angvel, p.w_accel) == (0.1, 0.5, 100, 100, 1, 100, 50)
     assert (p.tol, p.max_iter, p.bound_relax_factor, p.mu_init) == (1e-8, 3000, 1e-8, 0.1)
+    # the reference's max_cpu_time and Ipopt 3.12's defaults for the line-search mechanisms
+    assert (p.max_cpu_time, p.acceptable_tol, p.acceptable_iter, p.max_soc, p.kappa_soc) == (0.5, 1e-6, 15, 4, 0.99)
+    assert (p.watchdog_shortened_iter_trigger, p.watchdog_trial_iter_max, p.max_soft_resto_iters) == (10, 3, 10)
+    assert (p.soft_resto_pderror_reduction_factor, p.obj_max_inc, p.max_filter_resets) == (0.9999, 5.0, 5)
     assert libmpcg.mpcg_params_plugin_default(C.byref(p)) == 0
     assert (p.ref_v, p.w_cte, p.w_accel_d, p.max_angvel) == (1.0, 1000, 10, 1.0)
     assert libmpcg.mpcg_params_set(C.byref(p), b"STEPS", 33.7) == 0 and p.steps == 33
@@ -75,14 +89,15 @@ def test_param_defaults_and_keys(libmpcg):
 
 
 def test_workspace_bytes(libmpcg):
+    """Spill areas (114 N doubles per problem) plus the solve-order buffers beyond 2048."""
     from mpc_ros_amd import _lib
 
     p = _lib.MpcgParams()
     libmpcg.mpcg_params_plugin_default(C.byref(p))
-    b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)  # one 64-problem wavefront tile
-    assert b1 > 0 and libmpcg.mpcg_workspace_bytes(C.byref(p), 64) == b1
-    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65) == 2 * b1
-    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) == 1024 * b1
+    b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
+    assert b1 == 114 * 20 * 8
+    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 2048) == 2048 * b1
+    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) > 65536 * b1
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
 
 

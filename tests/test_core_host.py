@@ -1,9 +1,10 @@
 """Algorithm check of the device solver core on the CPU (no GPU needed).
 
-tests/native/ipm_host_check.cpp compiles mpc_ros_amd/csrc/ipm_core.h -- the exact
-code the HIP kernel runs per lane -- for the host, into a temporary directory (it is
-never part of the product).  Its results must equal the oracle's fixtures: the
-structured Riccati IPM follows the dense Ipopt restatement iterate for iterate.
+tests/native/wide_host_check.cpp compiles mpc_ros_amd/csrc/wide_core.h -- the exact
+code the HIP kernel runs, one problem per wavefront -- for the host, with 64 threads
+standing in for the lanes, into a temporary directory (it is never part of the
+product).  Its results must equal the oracle's fixtures: the structured Riccati IPM
+follows the dense Ipopt restatement iterate for iterate.
 """
 from __future__ import annotations
 
@@ -16,20 +17,25 @@ import pytest
 from conftest import ROOT, params_from_array
 
 
-@pytest.fixture(scope="module")
-def harness(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("hc") / "ipm_host_check")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-w", "-o", exe,
-                           os.path.join(ROOT, "tests", "native", "ipm_host_check.cpp")])
-    return exe
+def opts_line(o) -> str:
+    """The harness's Ipopt-option line from an oracle IpmOpts (same values both sides)."""
+    return (f"{o.acceptable_tol!r} {o.acceptable_iter} {o.acceptable_dual_inf_tol!r} {o.acceptable_constr_viol_tol!r} "
+            f"{o.acceptable_compl_inf_tol!r} {o.acceptable_obj_change_tol!r} {o.max_soc} {o.kappa_soc!r} "
+            f"{o.watchdog_shortened_iter_trigger} {o.watchdog_trial_iter_max} "
+            f"{o.soft_resto_pderror_reduction_factor!r} {o.max_soft_resto_iters} {o.obj_max_inc!r} "
+            f"{o.max_filter_resets} {o.filter_reset_trigger} {o.tiny_step_tol!r} {o.tiny_step_y_tol!r} "
+            f"{o.cpu_iter_budget} 64")
 
 
-def run_harness(exe, P, state, coeffs, tol=1e-8, max_iter=3000):
+def run_harness(exe, P, state, coeffs, opts=None):
+    from oracle import pyoracle as O
+
     N = int(P["STEPS"])
+    o = opts if opts is not None else O.ref_opts(N)
     hdr = (f"{N} {P['DT']!r} {P['REF_CTE']!r} {P['REF_ETHETA']!r} {P['REF_V']!r} {P['W_CTE']!r} {P['W_EPSI']!r} "
            f"{P['W_V']!r} {P['W_ANGVEL']!r} {P['W_A']!r} {P['W_DANGVEL']!r} {P['W_DA']!r} {P['ANGVEL']!r} "
-           f"{P['MAXTHR']!r} {P['BOUND']!r} {tol!r} {max_iter}\n{int(P.get('MODEL', 0))} {float(P.get('LF', 0.5))!r}\n"
-           f"{len(state)}\n")
+           f"{P['MAXTHR']!r} {P['BOUND']!r} {o.tol!r} {o.max_iter}\n{int(P.get('MODEL', 0))} {float(P.get('LF', 0.5))!r}\n"
+           f"{opts_line(o)}\n{len(state)}\n")
     body = "\n".join(" ".join(repr(float(v)) for v in np.concatenate([state[b], coeffs[b]]))
                      for b in range(len(state)))
     out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True).stdout
@@ -39,24 +45,20 @@ def run_harness(exe, P, state, coeffs, tol=1e-8, max_iter=3000):
 
 
 def compare(r, g, atol=1e-9):
-    np.testing.assert_array_equal(r["status"], g["status"])
-    np.testing.assert_array_equal(r["iters"], g["iters"])
-    np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=atol)
-    np.testing.assert_allclose(r["traj"], g["traj"], rtol=0, atol=atol)
-    np.testing.assert_allclose(r["obj"], g["obj"], rtol=1e-10, atol=1e-9)
-
-
-def test_core_matches_oracle_infinity_set(harness, infinity_golden):
-    g = infinity_golden
-    r = run_harness(harness, params_from_array(g["params"]), g["state"], g["coeffs"])
-    compare(r, g)
-
-
-@pytest.mark.parametrize("name", ["class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound"])
-def test_core_matches_oracle_variants(harness, variants_golden, name):
-    g = variants_golden[name]
-    r = run_harness(harness, params_from_array(g["params"]), g["state"], g["coeffs"])
-    compare(r, g)
+    """Same status and iteration count, values to rounding.  Rows on which the oracle
+    entered the feasibility-restoration phase (diag[:, 3] > 0) must end with
+    restoration_failure (9) on the device core, which has no restoration phase yet
+    (DESIGN.md); they are excluded from the value comparison."""
+    d = g.get("diag")
+    rs = np.zeros(len(g["status"]), bool) if d is None else d[:, 3] > 0
+    np.testing.assert_array_equal(r["status"][rs], 9)
+    k = ~rs
+    np.testing.assert_array_equal(r["status"][k], g["status"][k])
+    np.testing.assert_array_equal(r["iters"][k], g["iters"][k])
+    np.testing.assert_allclose(r["u0"][k], g["u0"][k], rtol=0, atol=atol)
+    np.testing.assert_allclose(r["traj"][k], g["traj"][k], rtol=0, atol=atol)
+    fin = k & np.isfinite(g["obj"])  # (the objective at a non-finite input is not compared)
+    np.testing.assert_allclose(r["obj"][fin], g["obj"][fin], rtol=1e-10, atol=1e-9)
 
 
 # ---------------------------------------------------------------- wavefront solver
@@ -75,16 +77,36 @@ def wide_harness(tmp_path_factory):
 def test_wide_core_matches_oracle_infinity_subset(wide_harness, infinity_golden):
     g = infinity_golden
     sel = np.r_[0:24, 256:264]  # course samples + edge cases
-    sub = {k: g[k][sel] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    sub = {k: g[k][sel] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["N20", "N40", "bicycle"])
+def test_wide_core_ipopt_features(wide_harness, features_golden, name):
+    """Second-order corrections, the watchdog and soft restoration: the device core takes
+    the oracle's path iterate for iterate (tests/golden/ipopt_features.npz)."""
+    g = features_golden[name]
+    r = run_harness(wide_harness, g["P"], g["state"], g["coeffs"])
+    compare(r, g, atol=1e-9)
+
+
+def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
+    """max_cpu_time as an iteration budget: status 14 (unknown) beyond it, as the oracle."""
+    g = features_golden["budget"]
+    sel = np.arange(8)
+    sub = {k: g[k][sel] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
+    r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"],
+                    opts=oracle.ref_opts(20, cpu_iter_budget=int(g["iter_budget"])))
+    compare(r, sub, atol=1e-9)
+    assert (r["status"] == 14).any()
 
 
 @pytest.mark.parametrize("name", ["class_defaults", "rate_w", "N40", "N3", "small_bound"])
 def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
     g = variants_golden[name]
     n = 6
-    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
 
@@ -93,13 +115,13 @@ def test_wide_core_bicycle_matches_oracle(wide_harness, bicycle_golden):
     """Kinematic-bicycle variant (N = 25) through the wavefront solver."""
     g = bicycle_golden
     n = 12
-    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters")}
+    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
 
 
 def _oracle_run(oracle, P, state, coeffs):
-    return oracle.mpc_solve_batch(P, state, coeffs, opts=oracle.ipm_opts(tol=1e-8), nthreads=4)
+    return oracle.mpc_solve_batch(P, state, coeffs, opts=oracle.ref_opts(int(P["STEPS"])), nthreads=4, diag=True)
 
 
 def test_wide_core_full_width_N64(wide_harness, oracle):
@@ -128,10 +150,10 @@ def nonfinite_inputs():
     return st, cf
 
 
-def test_nonfinite_inputs_stop_with_invalid_number(harness, wide_harness, oracle):
+def test_nonfinite_inputs_stop_with_invalid_number(wide_harness, oracle):
     """A non-finite f or g at the starting point ends the solve before the first
     iteration with Ipopt's INVALID_NUMBER_DETECTED (11) -- no hang, no iterations --
-    in the oracle and in both device cores; finite rows are unaffected."""
+    in the oracle and in the device core; finite rows are unaffected."""
     from mpc_ros_amd import params
 
     P = params.PLUGIN_DEFAULTS
@@ -140,8 +162,5 @@ def test_nonfinite_inputs_stop_with_invalid_number(harness, wide_harness, oracle
     np.testing.assert_array_equal(g["status"][[0, 1, 3, 4]], 11)
     np.testing.assert_array_equal(g["iters"][[0, 1, 3, 4]], 0)
     assert g["status"][5] == 1
-    for exe in (harness, wide_harness):
-        r = run_harness(exe, P, st, cf)
-        np.testing.assert_array_equal(r["status"], g["status"])
-        np.testing.assert_array_equal(r["iters"], g["iters"])
-        np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=1e-9)
+    r = run_harness(wide_harness, P, st, cf)
+    compare(r, g, atol=1e-9)

@@ -31,7 +31,7 @@ def _worker(rank, world, port, out_path):
         return torch.from_numpy(st), torch.from_numpy(cf)
 
     def solve(st, cf):
-        r = O.mpc_solve_batch(P, st.numpy(), cf.numpy(), opts=O.ipm_opts(tol=1e-8), nthreads=1)
+        r = O.mpc_solve_batch(P, st.numpy(), cf.numpy(), opts=O.ref_opts(int(P["STEPS"])), nthreads=1)
         return torch.from_numpy(r["u0"]), torch.from_numpy(r["status"])
 
     u0, status = D.solve_sharded(TOTAL, solve, make_inputs)
@@ -50,7 +50,7 @@ def test_two_rank_shard_and_gather(tmp_path, oracle):
     from mpc_ros_amd import infinity, params
 
     st, cf = infinity.make_problems(np.arange(TOTAL))
-    ref = oracle.mpc_solve_batch(params.PLUGIN_DEFAULTS, st, cf, opts=oracle.ipm_opts(tol=1e-8))
+    ref = oracle.mpc_solve_batch(params.PLUGIN_DEFAULTS, st, cf, opts=oracle.ref_opts(20))
     with np.load(out) as z:
         np.testing.assert_array_equal(z["status"], ref["status"])
         np.testing.assert_array_equal(z["u0"], ref["u0"])

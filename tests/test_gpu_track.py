@@ -127,7 +127,7 @@ def test_track_tick_matches_oracle_pipeline(torch_cuda, oracle):
         assert rc == 0
         sts.append(ost)
         cfs.append(ocf)
-    ref = oracle.mpc_solve_batch(P, np.array(sts), np.array(cfs), opts=oracle.ipm_opts(tol=1e-8), nthreads=16)
+    ref = oracle.mpc_solve_batch(P, np.array(sts), np.array(cfs), opts=oracle.ref_opts(int(P["STEPS"])), nthreads=16)
     w = ref["u0"][:, 0]
     thr = ref["u0"][:, 1]
     speed = np.minimum(vel[:, 0] + thr * P["DT"], P["REF_V"])

@@ -63,7 +63,7 @@ def test_oracle_reproduces_fixtures(oracle, infinity_golden):
     g = infinity_golden
     P = params_from_array(g["params"])
     sel = np.r_[0:24, 256:264]
-    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ipm_opts(tol=1e-8))
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ref_opts(int(P["STEPS"])))
     np.testing.assert_array_equal(r["status"], g["status"][sel])
     np.testing.assert_array_equal(r["iters"], g["iters"][sel])
     np.testing.assert_allclose(r["u0"], g["u0"][sel], rtol=0, atol=1e-12)
@@ -87,7 +87,7 @@ def test_golden_solutions_are_kkt_points(oracle, infinity_golden):
 
 
 def full_primal(oracle, P, state, coeffs, traj, u0):
-    r = oracle.mpc_solve(P, state, coeffs, opts=oracle.ipm_opts(tol=1e-8), full=True)
+    r = oracle.mpc_solve(P, state, coeffs, opts=oracle.ref_opts(int(P["STEPS"])), full=True)
     if np.abs(r["traj"] - traj).max() > 1e-12:
         return None
     return r["x"]
@@ -153,13 +153,46 @@ def test_bicycle_fixtures_reproduce_and_certify(oracle, bicycle_golden):
     g = bicycle_golden
     P = g["P"]
     sel = np.arange(0, 64, 4)
-    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ipm_opts(tol=1e-8))
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=oracle.ref_opts(int(P["STEPS"])))
     np.testing.assert_array_equal(r["status"], g["status"][sel])
     np.testing.assert_array_equal(r["iters"], g["iters"][sel])
     np.testing.assert_allclose(r["u0"], g["u0"][sel], rtol=0, atol=1e-12)
     for b in sel[:6]:
         if g["status"][b] != 1:
             continue
-        full = oracle.mpc_solve(P, g["state"][b], g["coeffs"][b], opts=oracle.ipm_opts(tol=1e-8), full=True)
+        full = oracle.mpc_solve(P, g["state"][b], g["coeffs"][b], opts=oracle.ref_opts(int(P["STEPS"])), full=True)
         res = oracle.mpc_kkt_residual(P, g["state"][b], g["coeffs"][b], full["x"])
         assert res["primal"] < 1e-8 and res["bound"] <= 1e-12
+
+
+def test_oracle_ipopt_mechanisms_fire_and_reproduce(oracle, features_golden):
+    """The fixture of Ipopt's mechanisms (second-order corrections, watchdog, soft
+    restoration, restoration phase) reproduces, and every mechanism acts on some problem;
+    the results of problems that went through the restoration phase are KKT points."""
+    seen = np.zeros(4, bool)
+    for name in ("N20", "N40", "bicycle"):
+        g = features_golden[name]
+        P = g["P"]
+        r = oracle.mpc_solve_batch(P, g["state"], g["coeffs"], opts=oracle.ref_opts(int(P["STEPS"])), diag=True)
+        np.testing.assert_array_equal(r["status"], g["status"])
+        np.testing.assert_array_equal(r["iters"], g["iters"])
+        np.testing.assert_array_equal(r["diag"], g["diag"])
+        np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=1e-12)
+        seen |= (g["diag"][:, :4] > 0).any(0)
+        for b in np.where(g["diag"][:, 3] > 0)[0][:3]:
+            full = oracle.mpc_solve(P, g["state"][b], g["coeffs"][b], opts=oracle.ref_opts(int(P["STEPS"])), full=True)
+            res = oracle.mpc_kkt_residual(P, g["state"][b], g["coeffs"][b], full["x"])
+            assert res["primal"] < 1e-8 and res["dual"] < 1e-5
+    assert seen.all(), seen
+
+
+def test_oracle_cpu_time_budget(oracle, features_golden):
+    """max_cpu_time 0.5 s (mpc_planner.cpp:368) as an iteration budget: > max_iter-free
+    problems stop with unknown (14) once iter exceeds it (solve_callback.hpp:1165-1167)."""
+    assert oracle.cpu_iter_budget(0.5, 20) == 2215 and oracle.cpu_iter_budget(1e6, 20) == -1
+    g = features_golden["budget"]
+    r = oracle.mpc_solve_batch(g["P"], g["state"], g["coeffs"],
+                               opts=oracle.ref_opts(20, cpu_iter_budget=int(g["iter_budget"])))
+    np.testing.assert_array_equal(r["status"], g["status"])
+    assert set(np.unique(r["status"])) == {1, 14}
+    assert r["iters"][r["status"] == 14].min() == int(g["iter_budget"]) + 1
