@@ -80,7 +80,8 @@ struct WideLayout {
     MPCG_HD int ZB() const { return RSC() + 16; }            // 8 zeros (an absent column)
     MPCG_HD int FI() const { return RSC() + 24; }
     MPCG_HD int C0() const { return FI() + 2 * cap; }  // -c of the initial-state rows (6) + pad
-    MPCG_HD int total() const { return C0() + 8; }
+    MPCG_HD int CTL() const { return C0() + 8; }       // 16 wave-uniform solver scalars (WideSolver::CtlRef)
+    MPCG_HD int total() const { return CTL() + 16; }
     // Per-problem HBM spill area (doubles) of the rare paths: the watchdog's stored iterate
     // and direction (LDS [W(0), YP(N)) = 52N), the last acceptable iterate (W: 10N), the
     // Newton direction kept while second-order corrections are tried (DW, YP: 16N), the
@@ -112,18 +113,50 @@ struct WideSolver {
     // statistics of the current iterate
     T fval, logsum, theta, prim_inf, prim_uns, dual_inf, compl0, pmin, pmax, l1y, l1z;
     // line-search / iteration state
-    T theta_max, theta_min, dw_last, acc_alpha, acc_z, kkt, delta_w_used;
+    T theta_min, dw_last, acc_alpha, acc_z, delta_w_used;
     int iter, nf, status;
     bool acc_pending;  // a step (acc_alpha, acc_z) waits to be applied by the next statistics sweep
     // filter line-search acceptor (Ipopt FilterLSAcceptor): reference point, switching-
     // condition powers (-gd)^s_phi and theta^s_theta of the reference, reset heuristic
-    T ref_theta, ref_phi, ref_gd, ref_pgd, ref_pth;
+    T ref_theta, ref_phi, ref_gd, ref_pgd, ref_pth, ref_inc;
     int last_rej_filter, count_filter_rej, n_filter_resets;
     // watchdog, tiny steps, soft restoration, acceptable points (BacktrackingLineSearch,
     // OptimalityErrorConvergenceCheck)
     int in_wd, wd_short, wd_trial_iter, tiny_last, tiny_flag, in_soft, soft_count, acc_counter, have_acc;
-    T wd_alpha_test, wd_theta, wd_phi, wd_gd, wd_amax_z, last_mu, last_obj, curr_obj;
+
     double* spill;  // this problem's HBM spill area (WideLayout::spill() doubles)
+    // Rarely used wave-uniform solver state lives in the problem's LDS control block
+    // (registers are the scarcer resource: every scalar held across the iteration loop
+    // competes with the sweeps).  x() = v stores (lane 0), x() reads (uniform).
+    struct CtlRef {
+        const WideSolver* s;
+        int i;
+        MPCG_HD operator T() const { return s->wv.uni_d(s->ld(s->L.CTL() + i)); }
+        MPCG_HD CtlRef& operator=(T v) {
+            s->wv.sync();
+            if (s->wv.lane() == 0) s->st(s->L.CTL() + i, v);
+            s->wv.sync();
+            return *this;
+        }
+        MPCG_HD CtlRef& operator=(const CtlRef& o) { return *this = (T)o; }  // (the value, not the binding)
+    };
+    MPCG_HD CtlRef wd_alpha_test() const { return CtlRef{this, 0}; }
+    MPCG_HD CtlRef wd_theta() const { return CtlRef{this, 1}; }
+    MPCG_HD CtlRef wd_phi() const { return CtlRef{this, 2}; }
+    MPCG_HD CtlRef wd_gd() const { return CtlRef{this, 3}; }
+    MPCG_HD CtlRef wd_amax_z() const { return CtlRef{this, 4}; }
+    MPCG_HD CtlRef soc_alpha() const { return CtlRef{this, 5}; }
+    MPCG_HD CtlRef soc_amax_z() const { return CtlRef{this, 6}; }
+    MPCG_HD CtlRef soc_theta_old() const { return CtlRef{this, 7}; }
+    MPCG_HD CtlRef soc_theta_trial() const { return CtlRef{this, 8}; }
+    MPCG_HD CtlRef soft_ec() const { return CtlRef{this, 9}; }
+    MPCG_HD CtlRef soft_a() const { return CtlRef{this, 10}; }
+    MPCG_HD CtlRef last_obj() const { return CtlRef{this, 11}; }
+    MPCG_HD CtlRef curr_obj() const { return CtlRef{this, 12}; }
+    MPCG_HD CtlRef kkt() const { return CtlRef{this, 13}; }
+    MPCG_HD CtlRef theta_max() const { return CtlRef{this, 14}; }
+    MPCG_HD CtlRef last_mu() const { return CtlRef{this, 15}; }
+
     // SPLIT: the sine/cosine pair of the last trial point (the lane's heading theta or
     // etheta), which the next statistics sweep reuses when that trial point was
     // accepted (the accepted iterate is bitwise the trial point: both are w + alpha dw)
@@ -131,7 +164,9 @@ struct WideSolver {
     int c_ok = 0;
     // SPLIT: reciprocal slacks 1/(w - lo), 1/(hi - w) of the lane's four variables, from
     // the stage data of the Newton system (same iterate) to the step statistics
+#ifdef MPCG_RD_CACHE
     T c_rdl[4] = {0, 0, 0, 0}, c_rdu[4] = {0, 0, 0, 0};
+#endif
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
@@ -768,8 +803,10 @@ struct WideSolver {
                 const T hb = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
                 if (mode == 0) {
                     const T rdl = rcp(w[q] - lo), rdu = rcp(hb - w[q]);
+#ifdef MPCG_RD_CACHE
                     c_rdl[q] = rdl;
                     c_rdu[q] = rdu;
+#endif
                     qd = sf * hq + zl[q] * rdl + zu[q] * rdu + delta_w;
                     qv = sf * gq - mu * rdl + mu * rdu;
                 } else {
@@ -1093,8 +1130,13 @@ struct WideSolver {
         for (int q = 0; q < 4; ++q) {
             if (q < nv) {
                 const T lo = q < 2 ? sl : (q == 2 ? lo2 : lo3), up_ = q < 2 ? su : (q == 2 ? hi2 : hi3);
-                const T gphi = gq[q] - mu * c_rdl[q] + mu * c_rdu[q];
-                dir_var_r(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], c_rdl[q], c_rdu[q], F);
+#ifdef MPCG_RD_CACHE
+                const T rdl = c_rdl[q], rdu = c_rdu[q];
+#else
+                const T rdl = rcp(w[q] - lo), rdu = rcp(up_ - w[q]);
+#endif
+                const T gphi = gq[q] - mu * rdl + mu * rdu;
+                dir_var_r(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], rdl, rdu, F);
             }
         }
     }
@@ -1465,6 +1507,11 @@ struct WideSolver {
         ref_gd = wv.uni_d(gd);
         ref_pgd = 0;
         ref_pth = 0;
+        // obj_max_inc: a trial barrier value more than 10^(obj_max_inc basval) above the
+        // reference is rejected (log10(phi_t - phi_ref) > obj_max_inc basval, evaluated once
+        // per search as the threshold)
+        const T basval = fabs(ref_phi) > (T)10 ? (T)log10((double)fabs(ref_phi)) : (T)1;
+        ref_inc = wv.uni_d((T)pow(10.0, (double)((T)P.obj_max_inc * basval)));
         if (wv.uni(gd < 0)) {
             ref_pgd = wv.uni_d((T)pow((double)-gd, 2.3));
             ref_pth = wv.uni_d((T)pow((double)th, 1.1));
@@ -1476,10 +1523,7 @@ struct WideSolver {
     }
     MPCG_HD bool acceptable_to_current_iterate(T phit, T thetat) const {
         const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8;
-        if (phit > ref_phi) {  // obj_max_inc
-            const T basval = fabs(ref_phi) > (T)10 ? (T)log10((double)fabs(ref_phi)) : (T)1;
-            if ((T)log10((double)(phit - ref_phi)) > (T)P.obj_max_inc * basval) return false;
-        }
+        if (phit > ref_phi && phit - ref_phi > ref_inc) return false;  // obj_max_inc
         return compare_le(thetat, ((T)1 - gamma_theta) * ref_theta, ref_theta) ||
                compare_le(phit - ref_phi, -gamma_phi * ref_theta, ref_phi);
     }
@@ -1546,9 +1590,9 @@ struct WideSolver {
     }
     // FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (with the filter reset heuristic)
     MPCG_HD bool check_acceptability(T alpha_test, T phit, T thetat) {
-        if (theta_max < 0) theta_max = wv.uni_d((T)1e4 * tmax((T)1, ref_theta));
+        if (theta_max() < 0) theta_max() = wv.uni_d((T)1e4 * tmax((T)1, ref_theta));
         if (theta_min < 0) theta_min = wv.uni_d((T)1e-4 * tmax((T)1, ref_theta));
-        if (wv.uni(thetat > theta_max)) return false;
+        if (wv.uni(thetat > theta_max())) return false;
         bool accept;
         if (alpha_test > 0 && is_ftype(alpha_test) && ref_theta <= theta_min)
             accept = armijo_holds(alpha_test, phit);
@@ -1592,145 +1636,7 @@ struct WideSolver {
         return (T)0.05 * a;
     }
 
-    // ------------------------------------------------------------ phases
-    MPCG_HD void init() {
-        setup();
-        init_point();
-        mu = wv.uni_d((T)P.mu_init);
-        tau = wv.uni_d(tmax((T)0.99, (T)1 - (T)P.mu_init));
-        status = 0;
-        // least-squares multipliers (constr_mult_init_max 1000)
-        const bool ok = riccati(1, (T)0);
-        T ymax = 0;
-        if (ok) {
-            forward(1);
-            wv.sync();
-            T m = 0;
-            if (t < N) {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) * rcp(rowscale(j, t))));
-            }
-            ymax = rmax(m);
-        }
-        const bool use = ok && ymax <= (T)1000;
-        wv.sync();
-        if (t < N) {
-#pragma unroll
-            for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
-        }
-        theta_max = -1;
-        theta_min = -1;
-        dw_last = 0;
-        delta_w_used = 0;
-        acc_alpha = 0;
-        acc_z = 0;
-        acc_pending = false;
-        iter = 0;
-        nf = 0;
-        kkt = 0;
-        ref_theta = ref_phi = ref_gd = ref_pgd = ref_pth = 0;
-        last_rej_filter = count_filter_rej = n_filter_resets = 0;
-        in_wd = wd_short = wd_trial_iter = tiny_last = tiny_flag = in_soft = soft_count = acc_counter = have_acc = 0;
-        wd_alpha_test = wd_theta = wd_phi = wd_gd = wd_amax_z = 0;
-        last_mu = -1;
-        last_obj = 0;
-        curr_obj = (T)-1e50;
-        cur_acceptable = false;
-    }
-
-    bool cur_acceptable;
-    // Convergence (OptimalityErrorConvergenceCheck::CheckConvergence) and the monotone
-    // barrier update (MonotoneMuUpdate::UpdateBarrierParameter) at the current iterate.
-    MPCG_HD int begin() {
-        stats(acc_pending, acc_alpha, acc_z);
-        acc_pending = false;
-        const int nbnd = 2 * (8 * N - 2);
-        const int ng = 6 * N;
-        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
-        const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
-        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
-        // unscaled_curr_dual_infeasibility / _complementarity: objective scaling undone
-        const T dual_uns = dual_inf / sf, compl_uns = compl0 / sf;
-        kkt = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl_uns)));
-        // CurrentIsAcceptable (objective bookkeeping once per iteration)
-        last_obj = curr_obj;
-        curr_obj = wv.uni_d(sf * fval);
-        cur_acceptable = wv.uni(E0 <= (T)P.acceptable_tol && dual_uns <= (T)P.acceptable_dual_inf_tol &&
-                                prim_uns <= (T)P.acceptable_constr_viol_tol &&
-                                compl_uns <= (T)P.acceptable_compl_inf_tol &&
-                                fabs(last_obj - curr_obj) / tmax((T)1, (T)fabs(curr_obj)) <=
-                                    (T)P.acceptable_obj_change_tol);
-        int s = 0;
-        // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
-        // drop a NaN; the sums do not)
-        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval)) {
-            s = IPM_INVALID_NUMBER;
-        } else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl_uns <= (T)1e-4) {
-            s = IPM_SUCCESS;
-        } else {
-            if (P.acceptable_iter > 0 && cur_acceptable) {
-                if (++acc_counter >= P.acceptable_iter) s = IPM_ACCEPTABLE;
-            } else {
-                acc_counter = 0;
-            }
-            if (!s && iter >= P.max_iter) s = IPM_MAXITER;
-            if (!s && P.cpu_iter_budget >= 0 && iter > P.cpu_iter_budget) s = IPM_UNKNOWN;
-        }
-        s = wv.uni(s);
-        if (s) return s;
-        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
-        const T mu_min = (T)(fmin(P.tol, 1e-4) / 11.0);  // min(tol, compl_inf_tol) / (kappa_eps + 1)
-        int tf = tiny_flag;
-        tiny_flag = 0;
-        bool done = false;
-        T complmu = tmax(pmax - mu, mu - pmin);
-        T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
-        while (wv.uni((Emu <= kappa_eps * mu || tf) && !done)) {
-            const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
-            const bool changed = mnew != mu;
-            if (!changed && tf) return IPM_TINY_STEP;
-            mu = mnew;
-            tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
-            if (!changed) {
-                done = true;
-            } else {
-                complmu = tmax(pmax - mu, mu - pmin);
-                Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
-                done = Emu > kappa_eps * mu;
-            }
-            if (done && changed) {  // BacktrackingLineSearch::Reset
-                in_soft = 0;
-                in_wd = 0;
-                wd_short = 0;
-                nf = 0;
-            }
-            tf = 0;
-        }
-        wv.mark(8);
-        return 0;
-    }
-
-    MPCG_HD int newton() {
-        T delta_w = 0;
-        int attempt = 0;
-        bool ok = false;
-        for (;;) {
-            if (riccati(0, delta_w)) {
-                ok = true;
-                if (delta_w > 0) dw_last = wv.uni_d(delta_w);
-                break;
-            }
-            if (attempt == 0)
-                delta_w = wv.uni_d((dw_last == 0) ? (T)1e-4 : tmax((T)1e-20, dw_last / (T)3));
-            else
-                delta_w = wv.uni_d((dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w);
-            ++attempt;
-            if (wv.uni(delta_w > (T)1e40)) break;
-        }
-        delta_w_used = delta_w;
-        return ok ? 0 : IPM_ERROR_IN_STEP;
-    }
-
+    // ------------------------------------------------------------ sweeps of the line search
     // Right-hand side of a second-order correction: d_soc = d(trial) + alpha d_soc, i.e.
     // c_soc = c(w + alpha dw) + alpha c_soc on the dynamics rows (stage table SD) and the
     // initial-state rows (C0); the trial point is the last one tried (W + alpha DW).
@@ -1771,104 +1677,6 @@ struct WideSolver {
             for (int j = 0; j < 6; ++j) st(L.C0() + j, c0[j] + alpha * ld(L.C0() + j));
         }
         wv.sync();
-    }
-
-    // FilterLSAcceptor::TrySecondOrderCorrection: up to max_soc corrected steps from the
-    // same factorisation (the Riccati sweep re-run on the same matrix with the corrected
-    // right-hand side); the Newton direction is kept in the spill area meanwhile.
-    MPCG_HD bool try_soc(T alpha_test, T& alpha, T& amax_z, T theta_trial) {
-        if (P.max_soc <= 0) return false;
-        spill_out(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
-        spill_out(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
-        int count = 0;
-        bool accept = false;
-        T theta_old = 0, alpha_soc = alpha;
-        while (wv.uni(count < P.max_soc && !accept && (count == 0 || theta_trial <= (T)P.kappa_soc * theta_old))) {
-            theta_old = theta_trial;
-            soc_rhs(alpha_soc);
-            riccati(0, delta_w_used);
-            const Fwd F2 = forward(0);
-            alpha_soc = F2.amax_p;
-            T phit, thetat;
-            const bool ok = trial(alpha_soc, &phit, &thetat);
-            accept = ok && check_acceptability(alpha_test, phit, thetat);
-            if (accept) {
-                alpha = alpha_soc;
-                amax_z = F2.amax_z;
-                update_for_next(alpha_test, phit);
-            } else {
-                ++count;
-                theta_trial = thetat;
-            }
-        }
-        if (!accept) {
-            spill_in(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
-            spill_in(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
-        }
-        return accept;
-    }
-
-    // BacktrackingLineSearch::DoBacktrackingLineSearch on the direction in DW / YP (its
-    // statistics F).  Returns whether a trial point was accepted; alpha, amax_z: the step.
-    MPCG_HD bool backtracking(const Fwd& F, bool skip_first, T& alpha, T& amax_z, int& n_steps, bool& eval_error) {
-        const T alpha_max = F.amax_p;
-        const T alpha_min = in_wd ? alpha_max : alpha_min_of();
-        alpha = alpha_max;
-        amax_z = F.amax_z;
-        T alpha_test = in_wd ? wd_alpha_test : alpha;
-        if (skip_first) alpha *= (T)0.5;
-        n_steps = 0;
-        eval_error = false;
-        bool accept = false;
-        c_ok = 0;
-        // (alpha halves towards alpha_min >= 0; the guard only bounds a zero alpha_min)
-        for (int guard = 0; guard < 1100; ++guard) {
-            if (!wv.uni(alpha > alpha_min || n_steps == 0)) break;
-            T phit, thetat;
-            const bool ok = trial(alpha, &phit, &thetat);
-            if (!in_wd) alpha_test = alpha;
-            if (ok) {
-                accept = check_acceptability(alpha_test, phit, thetat);
-            } else {
-                accept = false;
-                eval_error = true;
-            }
-            if (accept) {
-                update_for_next(alpha_test, phit);
-                break;
-            }
-            if (in_wd) break;
-            if (wv.uni(!eval_error && alpha == alpha_max && theta <= thetat)) {
-                accept = try_soc(alpha_test, alpha, amax_z, thetat);
-                if (accept) break;
-            }
-            alpha *= (T)0.5;
-            ++n_steps;
-        }
-        return accept;
-    }
-
-    MPCG_HD void start_watchdog(const Fwd& F) {
-        in_wd = 1;
-        spill_out(L.SP_WD(), 0, 52 * N);  // W, ZL, ZU, DW, Y, YP
-        wd_trial_iter = 0;
-        wd_alpha_test = F.amax_p;
-        wd_amax_z = F.amax_z;
-        wd_theta = ref_theta;
-        wd_phi = ref_phi;
-        wd_gd = ref_gd;
-    }
-    MPCG_HD void stop_watchdog(Fwd& F) {
-        in_wd = 0;
-        spill_in(L.SP_WD(), 0, 52 * N);
-        set_ref(wd_theta, wd_phi, wd_gd);
-        wd_short = 0;
-        F.amax_p = wd_alpha_test;
-        F.amax_z = wd_amax_z;
-        F.gd = wd_gd;
-        // statistics and stage data of the restored iterate
-        c_ok = 0;
-        stats(false, (T)0, (T)0);
     }
 
     // Primal-dual system error (1-norms of the dual infeasibility, the scaled constraint
@@ -1953,35 +1761,6 @@ struct WideSolver {
         }
         wv.sync();
     }
-    // BacktrackingLineSearch::TrySoftRestoStep: primal and dual step min(alpha_p, alpha_z),
-    // accepted by the original filter (sat) or by a reduction of the primal-dual error
-    MPCG_HD bool try_soft_resto(const Fwd& F, bool& sat) {
-        sat = false;
-        const T a = wv.uni_d(tmin(F.amax_p, F.amax_z));
-        T phit, thetat;
-        const bool ok = trial(a, &phit, &thetat);
-        if (!wv.uni(ok)) return false;
-        if (check_acceptability((T)0, phit, thetat)) {
-            sat = true;
-            acc_alpha = a;
-            acc_z = a;
-            acc_pending = true;
-            return true;
-        }
-        const T ec = pd_error();
-        spill_out(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);  // W, ZL, ZU
-        spill_out(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
-        accept_all(wv.lane(), true, a, a, false);
-        c_ok = 0;
-        const T et = pd_error();
-        if (wv.uni(et <= (T)P.soft_resto_factor * ec)) {
-            clamp_all();
-            return true;
-        }
-        spill_in(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);
-        spill_in(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
-        return false;
-    }
     // max |dy| of the direction (the tiny-step test's multiplier part)
     MPCG_HD T dy_max() {
         const int t = wv.lane();
@@ -1994,13 +1773,216 @@ struct WideSolver {
         return rmax(m);
     }
 
-    // BacktrackingLineSearch::FindAcceptableTrialPoint.  Returns 0 with the step to take
-    // pending (acc_*) or applied, or a termination status.
-    MPCG_HD int find_trial_point(Fwd F) {
-        if (mu != last_mu) {
+
+    // ------------------------------------------------------------ the solver as a state machine
+    // Every sweep (statistics, Newton system = Riccati + forward pass, trial point,
+    // second-order-correction right-hand side, primal-dual error) has exactly one call site
+    // in solve(); the control logic between sweeps -- Ipopt's convergence test, barrier
+    // update, inertia correction, filter line search with second-order corrections,
+    // watchdog and soft restoration -- runs as continuations (K_*) on wave-uniform values.
+    // (Inlined at several call sites the sweeps did not fit the register budget.)
+    enum Op : int { OP_STATS = 0, OP_SOLVE = 1, OP_TRIAL = 2, OP_PDERR = 3, OP_SOCRHS = 4 };
+    enum Ct : int {
+        K_LSQ = 0, K_BEGIN, K_NEWTON, K_BT, K_SOCRHS, K_SOC, K_SOC_TRIAL, K_SOFT_TRIAL, K_SOFT_PD0, K_SOFT_PD1,
+        K_WD_STATS
+    };
+    enum : int { LS_CONT = -1 };  // a continuation: the next sweep is set
+    int op, ct;
+    // operands and results of the sweeps
+    bool st_acc, sv_ok, tr_ok;
+    int sv_mode;
+    T st_alpha, st_z, sv_delta, tr_alpha, tr_test, tr_phi, tr_theta, pd_val;
+    bool tr_acc;  // the trial point passed CheckAcceptabilityOfTrialPoint(tr_test)
+    Fwd sv_F;
+    // line-search state (BacktrackingLineSearch)
+    Fwd lsF;  // statistics of the direction in DW / YP
+    T ls_alpha, ls_alpha_max, ls_alpha_min, ls_alpha_test, ls_amax_z;
+    int ls_n_steps, inertia_attempt, soft_ctx;
+    bool ls_eval_error, ls_skip_first, wd_from_tiny;
+    int soc_count;
+    bool cur_acceptable;
+
+    MPCG_HD int set_op(int o, int c) {
+        op = o;
+        ct = c;
+        return LS_CONT;
+    }
+    // a trial point, checked by the filter acceptor with step length alpha_test
+    MPCG_HD int do_trial(T alpha, T alpha_test, int c) {
+        tr_alpha = wv.uni_d(alpha);
+        tr_test = wv.uni_d(alpha_test);
+        return set_op(OP_TRIAL, c);
+    }
+    MPCG_HD int do_solve(int mode, T delta, int c) {
+        sv_mode = mode;
+        sv_delta = wv.uni_d(delta);
+        return set_op(OP_SOLVE, c);
+    }
+    MPCG_HD int do_stats(bool acc, T alpha, T z, int c) {
+        st_acc = acc;
+        st_alpha = alpha;
+        st_z = z;
+        return set_op(OP_STATS, c);
+    }
+
+    MPCG_HD void init() {
+        setup();
+        init_point();
+        mu = wv.uni_d((T)P.mu_init);
+        tau = wv.uni_d(tmax((T)0.99, (T)1 - (T)P.mu_init));
+        status = 0;
+        theta_max() = -1;
+        theta_min = -1;
+        dw_last = 0;
+        delta_w_used = 0;
+        acc_alpha = 0;
+        acc_z = 0;
+        acc_pending = false;
+        iter = 0;
+        nf = 0;
+        kkt() = 0;
+        ref_theta = ref_phi = ref_gd = ref_pgd = ref_pth = 0;
+        last_rej_filter = count_filter_rej = n_filter_resets = 0;
+        in_wd = wd_short = wd_trial_iter = tiny_last = tiny_flag = in_soft = soft_count = acc_counter = have_acc = 0;
+        wd_alpha_test() = wd_theta() = wd_phi() = wd_gd() = wd_amax_z() = 0;
+        last_mu() = -1;
+        last_obj() = 0;
+        curr_obj() = (T)-1e50;
+        cur_acceptable = false;
+        st_acc = sv_ok = tr_ok = false;
+        st_alpha = st_z = tr_alpha = tr_test = tr_phi = tr_theta = pd_val = 0;
+        tr_acc = false;
+        ls_alpha = ls_alpha_max = ls_alpha_min = ls_alpha_test = ls_amax_z = 0;
+        ls_n_steps = inertia_attempt = soft_ctx = 0;
+        ls_eval_error = ls_skip_first = wd_from_tiny = false;
+        soc_alpha() = soc_amax_z() = soc_theta_old() = soc_theta_trial() = soft_ec() = soft_a() = 0;
+        soc_count = 0;
+        lsF = Fwd{(T)1, (T)1, (T)0, (T)0};
+        sv_F = lsF;
+        // least-squares multipliers first (constr_mult_init_max 1000)
+        do_solve(1, (T)0, K_LSQ);
+    }
+
+    // K_LSQ: the least-squares multiplier estimate y0, used if |y0| <= 1000
+    MPCG_HD int k_lsq() {
+        T ymax = 0;
+        if (sv_ok) {
+            const int t = wv.lane();
+            wv.sync();
+            T m = 0;
+            if (t < N) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) * rcp(rowscale(j, t))));
+            }
+            ymax = rmax(m);
+        }
+        const bool use = sv_ok && ymax <= (T)1000;
+        {
+            const int t = wv.lane();
+            wv.sync();
+            if (t < N) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
+            }
+        }
+        return do_stats(false, (T)0, (T)0, K_BEGIN);
+    }
+
+    // K_BEGIN: convergence (OptimalityErrorConvergenceCheck::CheckConvergence) and the
+    // monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter) at the iterate
+    // the statistics sweep just evaluated; then the Newton system.
+    MPCG_HD int k_begin() {
+        acc_pending = false;
+        const int nbnd = 2 * (8 * N - 2);
+        const int ng = 6 * N;
+        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
+        const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
+        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
+        // unscaled_curr_dual_infeasibility / _complementarity: objective scaling undone
+        const T dual_uns = dual_inf / sf, compl_uns = compl0 / sf;
+        kkt() = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl_uns)));
+        // CurrentIsAcceptable (objective bookkeeping once per iteration)
+        last_obj() = curr_obj();
+        curr_obj() = wv.uni_d(sf * fval);
+        cur_acceptable = wv.uni(E0 <= (T)P.acceptable_tol && dual_uns <= (T)P.acceptable_dual_inf_tol &&
+                                prim_uns <= (T)P.acceptable_constr_viol_tol &&
+                                compl_uns <= (T)P.acceptable_compl_inf_tol &&
+                                fabs(last_obj() - curr_obj()) / tmax((T)1, (T)fabs(curr_obj())) <=
+                                    (T)P.acceptable_obj_change_tol);
+        int s = 0;
+        // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
+        // drop a NaN; the sums do not)
+        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval)) {
+            s = IPM_INVALID_NUMBER;
+        } else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl_uns <= (T)1e-4) {
+            s = IPM_SUCCESS;
+        } else {
+            if (P.acceptable_iter > 0 && cur_acceptable) {
+                if (++acc_counter >= P.acceptable_iter) s = IPM_ACCEPTABLE;
+            } else {
+                acc_counter = 0;
+            }
+            if (!s && iter >= P.max_iter) s = IPM_MAXITER;
+            if (!s && P.cpu_iter_budget >= 0 && iter > P.cpu_iter_budget) s = IPM_UNKNOWN;
+        }
+        s = wv.uni(s);
+        if (s) return s;
+        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
+        const T mu_min = (T)(fmin(P.tol, 1e-4) / 11.0);  // min(tol, compl_inf_tol) / (kappa_eps + 1)
+        int tf = tiny_flag;
+        tiny_flag = 0;
+        bool done = false;
+        T complmu = tmax(pmax - mu, mu - pmin);
+        T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+        while (wv.uni((Emu <= kappa_eps * mu || tf) && !done)) {
+            const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
+            const bool changed = mnew != mu;
+            if (!changed && tf) return IPM_TINY_STEP;
+            mu = mnew;
+            tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
+            if (!changed) {
+                done = true;
+            } else {
+                complmu = tmax(pmax - mu, mu - pmin);
+                Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+                done = Emu > kappa_eps * mu;
+            }
+            if (done && changed) {  // BacktrackingLineSearch::Reset
+                in_soft = 0;
+                in_wd = 0;
+                wd_short = 0;
+                nf = 0;
+            }
+            tf = 0;
+        }
+        wv.mark(8);
+        inertia_attempt = 0;
+        return do_solve(0, (T)0, K_NEWTON);
+    }
+
+    // K_NEWTON: inertia correction (Algorithm IC); once the system is solved, the line search
+    MPCG_HD int k_newton() {
+        if (!sv_ok) {
+            T delta_w = sv_delta;
+            if (inertia_attempt == 0)
+                delta_w = (dw_last == 0) ? (T)1e-4 : tmax((T)1e-20, dw_last / (T)3);
+            else
+                delta_w = (dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
+            ++inertia_attempt;
+            if (wv.uni(delta_w > (T)1e40)) return IPM_ERROR_IN_STEP;
+            return do_solve(0, delta_w, K_NEWTON);
+        }
+        if (sv_delta > 0) dw_last = sv_delta;
+        delta_w_used = sv_delta;
+        return ls_begin(sv_F);
+    }
+
+    // BacktrackingLineSearch::FindAcceptableTrialPoint, up to the backtracking search
+    MPCG_HD int ls_begin(Fwd F) {
+        if (mu != last_mu()) {
             in_wd = 0;
             wd_short = 0;
-            last_mu = mu;
+            last_mu() = mu;
         }
         if (P.acceptable_iter > 0 && cur_acceptable) {
             spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
@@ -2008,112 +1990,300 @@ struct WideSolver {
         }
         const T phik = wv.uni_d(sf * fval - mu * logsum);
         if (in_wd)
-            set_ref(wd_theta, wd_phi, wd_gd);
+            set_ref(wd_theta(), wd_phi(), wd_gd());
         else
             set_ref(theta, phik, F.gd);
-        bool accept = false, soft_or_resto = false;
-        int n_steps = 0;
-        T alpha = 0, amax_z = F.amax_z;
+        lsF = F;
         bool tiny = false;
         if (P.tiny_step_tol > 0 && wv.uni(F.rel <= (T)P.tiny_step_tol)) tiny = wv.uni(dy_max() <= (T)P.tiny_step_y_tol);
         if (in_wd && tiny) {
-            stop_watchdog(F);
-            tiny = false;
+            // the watchdog stops at a tiny step: back to its stored iterate, then the
+            // ordinary line search there
+            wd_from_tiny = true;
+            return stop_watchdog();
         }
-        if (P.watchdog_trigger > 0 && !in_wd && !tiny && !in_soft && wd_short >= P.watchdog_trigger) start_watchdog(F);
+        if (P.watchdog_trigger > 0 && !in_wd && !tiny && !in_soft && wd_short >= P.watchdog_trigger)
+            start_watchdog(F);
         if (tiny) {
-            alpha = F.amax_p;
-            amax_z = F.amax_z;
+            ls_alpha = F.amax_p;
+            ls_amax_z = F.amax_z;
+            ls_n_steps = 0;
             c_ok = 0;
             if (tiny_last) tiny_flag = 1;
             tiny_last = 1;
-            accept = true;
-        } else {
-            tiny_last = 0;
-            if (in_soft) {
-                if (++soft_count > P.max_soft_resto_iters) {
-                    accept = false;
-                } else {
-                    bool sat;
-                    accept = try_soft_resto(F, sat);
-                    if (accept && sat) {
-                        in_soft = 0;
-                        soft_count = 0;
-                    }
-                }
-                soft_or_resto = accept;
-            } else {
-                bool done = false, skip_first = false;
-                while (!done) {
-                    bool eval_error;
-                    accept = backtracking(F, skip_first, alpha, amax_z, n_steps, eval_error);
-                    if (in_wd) {
-                        if (accept) {
-                            in_wd = 0;
-                            done = true;
-                        } else {
-                            ++wd_trial_iter;
-                            if (eval_error || wd_trial_iter > P.watchdog_trial_max) {
-                                stop_watchdog(F);
-                                skip_first = true;
-                            } else {
-                                done = true;
-                                accept = true;
-                            }
-                        }
-                    } else {
-                        done = true;
-                    }
-                }
-            }
+            return ls_finish(true, false);
         }
+        tiny_last = 0;
+        if (in_soft) {
+            if (++soft_count > P.max_soft_resto_iters) return ls_finish(false, false);
+            soft_ctx = 0;
+            return soft_start();
+        }
+        ls_skip_first = false;
+        return bt_start();
+    }
+
+    // BacktrackingLineSearch::DoBacktrackingLineSearch on the direction lsF (DW / YP)
+    MPCG_HD int bt_start() {
+        ls_alpha_max = lsF.amax_p;
+        ls_alpha_min = in_wd ? ls_alpha_max : alpha_min_of();
+        ls_alpha = ls_alpha_max;
+        ls_amax_z = lsF.amax_z;
+        ls_alpha_test = in_wd ? wd_alpha_test() : ls_alpha;
+        if (ls_skip_first) ls_alpha *= (T)0.5;
+        ls_n_steps = 0;
+        ls_eval_error = false;
+        return bt_next();
+    }
+    MPCG_HD int bt_next() {
+        // (alpha halves towards alpha_min >= 0; the step bound only ends a zero alpha_min)
+        if (wv.uni((ls_alpha > ls_alpha_min || ls_n_steps == 0) && ls_n_steps < 1100)) {
+            if (!in_wd) ls_alpha_test = ls_alpha;
+            return do_trial(ls_alpha, ls_alpha_test, K_BT);
+        }
+        return bt_done(false);
+    }
+    // K_BT: a trial point of the backtracking search was evaluated
+    MPCG_HD int k_bt() {
+        const bool accept = tr_acc;
+        if (!tr_ok) ls_eval_error = true;
+        if (accept) {
+            update_for_next(ls_alpha_test, tr_phi);
+            return bt_done(true);
+        }
+        if (in_wd) return bt_done(false);
+        if (wv.uni(!ls_eval_error && ls_alpha == ls_alpha_max && theta <= tr_theta) && P.max_soc > 0) {
+            // FilterLSAcceptor::TrySecondOrderCorrection from the same factorisation; the
+            // Newton direction waits in the spill area
+            spill_out(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+            spill_out(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+            soc_count = 0;
+            soc_alpha() = ls_alpha;
+            soc_theta_old() = 0;
+            soc_theta_trial() = tr_theta;
+            return soc_next();
+        }
+        ls_alpha *= (T)0.5;
+        ++ls_n_steps;
+        return bt_next();
+    }
+    MPCG_HD int soc_next() {
+        if (wv.uni(soc_count < P.max_soc &&
+                   (soc_count == 0 || soc_theta_trial() <= (T)P.kappa_soc * soc_theta_old()))) {
+            soc_theta_old() = soc_theta_trial();
+            return set_op(OP_SOCRHS, K_SOCRHS);
+        }
+        spill_in(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+        spill_in(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+        ls_alpha *= (T)0.5;
+        ++ls_n_steps;
+        return bt_next();
+    }
+    // K_SOCRHS: c_soc written; solve with the same matrix (same delta_w)
+    MPCG_HD int k_socrhs() { return do_solve(0, delta_w_used, K_SOC); }
+    // K_SOC: the corrected step is in DW / YP
+    MPCG_HD int k_soc() {
+        soc_alpha() = wv.uni_d(sv_F.amax_p);
+        soc_amax_z() = wv.uni_d(sv_F.amax_z);
+        return do_trial(soc_alpha(), ls_alpha_test, K_SOC_TRIAL);
+    }
+    MPCG_HD int k_soc_trial() {
+        const bool accept = tr_acc;
+        if (accept) {
+            ls_alpha = soc_alpha();
+            ls_amax_z = soc_amax_z();
+            update_for_next(ls_alpha_test, tr_phi);
+            return bt_done(true);
+        }
+        ++soc_count;
+        soc_theta_trial() = tr_theta;
+        return soc_next();
+    }
+    // the watchdog around the backtracking search (FindAcceptableTrialPoint)
+    MPCG_HD int bt_done(bool accept) {
+        if (in_wd) {
+            if (accept) {
+                in_wd = 0;
+                return ls_finish(true, false);
+            }
+            ++wd_trial_iter;
+            if (ls_eval_error || wd_trial_iter > P.watchdog_trial_max) {
+                wd_from_tiny = false;
+                return stop_watchdog();
+            }
+            return ls_finish(true, false);  // the watchdog's unchecked step
+        }
+        return ls_finish(accept, false);
+    }
+    MPCG_HD void start_watchdog(const Fwd& F) {
+        in_wd = 1;
+        spill_out(L.SP_WD(), 0, 52 * N);  // W, ZL, ZU, DW, Y, YP
+        wd_trial_iter = 0;
+        wd_alpha_test() = F.amax_p;
+        wd_amax_z() = F.amax_z;
+        wd_theta() = ref_theta;
+        wd_phi() = ref_phi;
+        wd_gd() = ref_gd;
+    }
+    // back to the watchdog's stored iterate and direction; its statistics next
+    MPCG_HD int stop_watchdog() {
+        in_wd = 0;
+        spill_in(L.SP_WD(), 0, 52 * N);
+        wd_short = 0;
+        c_ok = 0;
+        return do_stats(false, (T)0, (T)0, K_WD_STATS);
+    }
+    MPCG_HD int k_wd_stats() {
+        set_ref(wd_theta(), wd_phi(), wd_gd());
+        lsF.amax_p = wd_alpha_test();
+        lsF.amax_z = wd_amax_z();
+        lsF.gd = wd_gd();
+        ls_skip_first = !wd_from_tiny;
+        return bt_start();
+    }
+
+    // BacktrackingLineSearch::TrySoftRestoStep: primal and dual step min(alpha_p, alpha_z),
+    // accepted by the original filter or by a reduction of the primal-dual error.
+    // soft_ctx 0: an iteration of the soft restoration phase; 1: its first step.
+    MPCG_HD int soft_start() {
+        soft_a() = wv.uni_d(tmin(lsF.amax_p, lsF.amax_z));
+        return do_trial(soft_a(), (T)0, K_SOFT_TRIAL);
+    }
+    MPCG_HD int k_soft_trial() {
+        if (!tr_ok) return soft_done(false, false);
+        if (tr_acc) {
+            acc_alpha = soft_a();
+            acc_z = soft_a();
+            acc_pending = true;
+            return soft_done(true, true);
+        }
+        return set_op(OP_PDERR, K_SOFT_PD0);
+    }
+    MPCG_HD int k_soft_pd0() {
+        soft_ec() = pd_val;
+        spill_out(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);  // W, ZL, ZU
+        spill_out(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        accept_all(wv.lane(), true, soft_a(), soft_a(), false);
+        c_ok = 0;
+        return set_op(OP_PDERR, K_SOFT_PD1);
+    }
+    MPCG_HD int k_soft_pd1() {
+        if (wv.uni(pd_val <= (T)P.soft_resto_factor * soft_ec())) {
+            // kappa_sigma correction of the accepted multipliers
+            const int t = wv.lane();
+            wv.sync();
+            const T bl[3] = {sl, wl, al}, bh[3] = {su, wu, au};
+            for (int e = t; e < 8 * N; e += 64) {
+                const int k = e >> 3, j = e & 7;
+                if (k == N - 1 && j >= 6) continue;
+                const T lo = j < 6 ? bl[0] : (j == 6 ? bl[1] : bl[2]);
+                const T hi = j < 6 ? bh[0] : (j == 6 ? bh[1] : bh[2]);
+                T zln, zun;
+                clamp_z(ld(L.W(k) + j), ld(L.ZL(k) + j), ld(L.ZU(k) + j), lo, hi, &zln, &zun);
+                st(L.ZL(k) + j, zln);
+                st(L.ZU(k) + j, zun);
+            }
+            wv.sync();
+            return soft_done(true, false);
+        }
+        spill_in(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);
+        spill_in(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        return soft_done(false, false);
+    }
+    MPCG_HD int soft_done(bool accept, bool sat) {
+        if (soft_ctx == 0) {  // an iteration of the soft restoration phase
+            if (accept && sat) {
+                in_soft = 0;
+                soft_count = 0;
+            }
+            return accept ? ls_done() : ls_fail();
+        }
+        if (accept) {  // the first step of the soft restoration phase
+            in_soft = !sat;
+            return ls_done();
+        }
+        return ls_fail();
+    }
+
+    // the end of FindAcceptableTrialPoint
+    MPCG_HD int ls_finish(bool accept, bool soft_or_resto) {
         if (!accept) {
             if (!in_soft && P.soft_resto_factor > 0) {
                 augment_filter();  // PrepareRestoPhaseStart
-                bool sat;
-                if (try_soft_resto(F, sat)) {
-                    in_soft = !sat;
-                    accept = true;
-                    soft_or_resto = true;
-                }
+                soft_ctx = 1;
+                return soft_start();
             }
-            if (!accept) {
-                if (!in_soft) augment_filter();
-                // almost feasible: the last acceptable iterate, if any, is the result
-                if (wv.uni(theta <= (T)1e-2 * (T)P.tol) && have_acc) {
-                    spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
-                    return IPM_ACCEPTABLE;
-                }
-                // Ipopt enters its feasibility restoration phase here (oracle/ipm.c
-                // perform_restoration); the device solver stops
-                return IPM_RESTORATION_FAILURE;
-            }
+            return ls_fail();
         }
         if (!soft_or_resto) {
-            acc_alpha = wv.uni_d(alpha);
-            acc_z = wv.uni_d(amax_z);
+            acc_alpha = wv.uni_d(ls_alpha);
+            acc_z = wv.uni_d(ls_amax_z);
             acc_pending = true;
-            if (n_steps == 0)
+            if (ls_n_steps == 0)
                 wd_short = 0;
             else
                 ++wd_short;
         }
+        return ls_done();
+    }
+    // the step is taken (pending or applied): the next iteration
+    MPCG_HD int ls_done() {
         wv.mark(7);
-        return 0;
+        ++iter;
+        return do_stats(acc_pending, acc_alpha, acc_z, K_BEGIN);
+    }
+    MPCG_HD int ls_fail() {
+        if (!in_soft) augment_filter();
+        // almost feasible: the last acceptable iterate, if any, is the result
+        if (wv.uni(theta <= (T)1e-2 * (T)P.tol) && have_acc) {
+            spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
+            return IPM_ACCEPTABLE;
+        }
+        // Ipopt enters its feasibility restoration phase here (oracle/ipm.c
+        // perform_restoration); the device solver stops
+        return IPM_RESTORATION_FAILURE;
+    }
+
+    MPCG_HD int step(int c) {
+        switch (c) {
+            case K_LSQ: return k_lsq();
+            case K_BEGIN: return k_begin();
+            case K_NEWTON: return k_newton();
+            case K_BT: return k_bt();
+            case K_SOCRHS: return k_socrhs();
+            case K_SOC: return k_soc();
+            case K_SOC_TRIAL: return k_soc_trial();
+            case K_SOFT_TRIAL: return k_soft_trial();
+            case K_SOFT_PD0: return k_soft_pd0();
+            case K_SOFT_PD1: return k_soft_pd1();
+            default: return k_wd_stats();
+        }
     }
 
     MPCG_HD void solve() {
         init();
         for (;;) {
-            int s = begin();
-            if (s) { status = s; break; }
-            s = newton();
-            if (s) { status = s; break; }
-            const Fwd F = forward(0);
-            s = find_trial_point(F);
-            if (s) { status = s; break; }
-            ++iter;
+            const int o = wv.uni(op);
+            if (o == OP_STATS) {
+                stats(st_acc, st_alpha, st_z);
+            } else if (o == OP_SOLVE) {
+                sv_ok = wv.uni(riccati(sv_mode, sv_delta));
+                if (sv_ok) sv_F = forward(sv_mode);
+            } else if (o == OP_TRIAL) {
+                tr_ok = trial(tr_alpha, &tr_phi, &tr_theta);
+                tr_acc = tr_ok && check_acceptability(tr_test, tr_phi, tr_theta);
+            } else if (o == OP_PDERR) {
+                pd_val = pd_error();
+            } else {
+                soc_rhs(soc_alpha());
+            }
+            const int s = step(wv.uni(ct));
+            if (s > 0) {
+                status = s;
+                break;
+            }
         }
+        // iter counts accepted steps
         wv.sync();
     }
 
