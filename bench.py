@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--model", default="diffdrive", choices=["diffdrive", "bicycle"],
                     help="dynamics: FG_eval's differential drive, or the kinematic bicycle (BASELINE configs[4]: "
                          "run with --horizon 25)")
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"],
+                    help="solver arithmetic: fp64 (the reference's) or the fp32 solver (BASELINE configs[2]: "
+                         "run with --horizon 40)")
     ap.add_argument("--selftest", action="store_true",
                     help="launch/shard/gather plumbing only: gloo on CPU, a stub solver that writes each "
                          "problem's global index (tests/test_bench_launch.py); no GPU, no timing claim")
@@ -69,14 +72,33 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """(threads available to this process, CPU model name)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the box's CPU share when set
+    threads = max(1, min(n, env) if env > 0 else n)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, model
+
+
 def cpu_baseline(P, st, cf, budget_s):
-    """Oracle (Ipopt restatement, dense KKT) timed on the host cores."""
+    """Oracle (Ipopt restatement, dense KKT) timed on the host cores this process may use."""
     from oracle import pyoracle as O
 
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    opts = O.ipm_opts(tol=1e-8)
+    threads, model = host_cpu()
+    opts = O.ref_opts(int(P["STEPS"]))
     n = threads * 2
     t0 = time.perf_counter()
     O.mpc_solve_batch(P, st[:n], cf[:n], opts=opts, nthreads=threads)
@@ -86,9 +108,10 @@ def cpu_baseline(P, st, cf, budget_s):
     t0 = time.perf_counter()
     r = O.mpc_solve_batch(P, st[:m], cf[:m], opts=opts, nthreads=threads)
     dt = time.perf_counter() - t0
-    return dict(value=m / dt, unit="solves/s", cores=threads, kind="port",
-                sample=f"first {m} problems of the benchmark batch, oracle/ipm.c (Ipopt 3.12 algorithm, dense "
-                       f"Bunch-Kaufman KKT), {threads} OpenMP threads, {dt:.1f} s",
+    return dict(value=m / dt, unit="solves/s", cores=threads, kind="port", cpu_model=model,
+                sample=f"first {m} problems of the benchmark batch, oracle/ipm.c (Ipopt 3.12 algorithm with SOC, "
+                       f"watchdog, restoration; dense Bunch-Kaufman KKT), {threads} OpenMP threads "
+                       f"(sched_getaffinity, capped by OMP_NUM_THREADS), {dt:.1f} s",
                 iters_mean=float(np.mean(r["iters"])))
 
 
@@ -115,7 +138,7 @@ def latency_b1(P, st, cf, solver, dev, reps=50):
         if r >= 5:
             dev_ms.append((t1 - t0) * 1e3)
             host_ms.append((t2 - t1) * 1e3)
-    opts = O.ipm_opts(tol=1e-8)
+    opts = O.ref_opts(int(P["STEPS"]))
     for r in range(min(reps, 20)):
         t0 = time.perf_counter()
         O.mpc_solve_batch(P, s1, c1, opts=opts, nthreads=1)
@@ -241,7 +264,7 @@ def main():
         tvel = torch.from_numpy(np.ascontiguousarray(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))).to(dev)
         tplan = torch.from_numpy(np.ascontiguousarray(plan)).to(dev)
         cmd = torch.empty((count, 3), dtype=torch.float64, device=dev)
-    solver = BatchSolver(dev.index, P, strategy=a.strategy)
+    solver = BatchSolver(dev.index, P, strategy=a.strategy, dtype=a.dtype)
     solver.reserve(count)
     u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
     traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)
@@ -296,7 +319,7 @@ def main():
         bytes_per_solve = 8 * (6 + 4 + 2 + 3 * N)
         achieved = count * bytes_per_solve / (kern * 1e-3) / 1e9
         prof = a.profile_name or f"pmc_B{B}_N{N}"
-        pmc = pmc_profile(prof) if solver.strategy == "wave" else {}
+        pmc = pmc_profile(prof) if a.dtype == "fp64" else {}
         traffic = pmc.get("hbm_bytes_per_launch")
         fl = pmc.get("fp64_flops_per_solve")
         valu = None
@@ -317,13 +340,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if a.dtype == "fp64" else "f32",
             "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem)",
             "config": {"workload": f"{'diff-drive' if a.model == 'diffdrive' else 'kinematic-bicycle'} NMPC "
-                                   f"(MPC::Solve NLP, Ipopt algorithm), N={N}, fp64, "
+                                   f"(MPC::Solve NLP, Ipopt algorithm), N={N}, {a.dtype}, "
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
                        "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}",
-                       "mode": a.mode, "model": a.model},
+                       "mode": a.mode, "model": a.model, "dtype": a.dtype},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mpcg::k_solve_wide" if solver.strategy == "wave" else "lane kernels",

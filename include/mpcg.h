@@ -88,6 +88,9 @@ typedef struct mpcg_params {
     double obj_max_inc;                /* 5 */
     double tiny_step_tol;              /* 10 eps */
     double tiny_step_y_tol;            /* 1e-2 */
+    double dual_inf_tol;               /* 1 (unscaled dual infeasibility at termination) */
+    double constr_viol_tol;            /* 1e-4 (unscaled constraint violation; caps the bound relaxation) */
+    double compl_inf_tol;              /* 1e-4 (unscaled complementarity; mu_min = min(tol, this) / 11) */
     int32_t acceptable_iter;           /* 15 (0: no acceptable termination) */
     int32_t max_soc;                   /* 4 (0: no second-order corrections) */
     int32_t watchdog_shortened_iter_trigger; /* 10 (0: no watchdog) */
@@ -95,7 +98,11 @@ typedef struct mpcg_params {
     int32_t max_soft_resto_iters;      /* 10 */
     int32_t max_filter_resets;         /* 5 */
     int32_t filter_reset_trigger;      /* 5 */
-    int32_t reserved;
+    /* Arithmetic of the solve: 0 = fp64 (the reference's double, the default); 1 = fp32
+     * (BASELINE configs[2]; differential drive only): iterate, multipliers and Newton systems
+     * in float -- state a tolerance a float iterate can meet (tol ~1e-5 instead of 1e-8;
+     * tiny_step_tol 10 FLT_EPSILON).  Inputs and outputs stay double. */
+    int32_t precision;
 } mpcg_params;
 
 typedef struct mpcg_handle mpcg_handle;
@@ -143,6 +150,16 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
  * allocation if mpcg_reserve(h, B) was called. */
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
+
+/* Multi-GPU batched solve from one process, host buffers as
+ * mpcg_solve: the B problems are split into ngpu contiguous shards (the first B % ngpu
+ * GPUs take one more), solved on devices[r] with the given parameters, and the results are
+ * gathered to devices[0] by grouped RCCL send/recv (one message per output array and GPU,
+ * point-to-point over xGMI), then copied to the host.  Creates and destroys its handles and
+ * communicator per call (a serving loop keeps per-GPU handles and gathers itself, as
+ * bench.py does with torch.distributed).  Returns 0, or < 0 (-4: RCCL). */
+int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
+                     const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters);
 
 /* Tracking::findBestPath's preprocessing (mpc_ros/src/driving_state.cpp:175-256) on the
  * device for B robots: waypoints to the vehicle frame, cubic polyfit (Householder QR),

@@ -33,10 +33,11 @@ class MpcgParams(C.Structure):
         ("acceptable_constr_viol_tol", C.c_double), ("acceptable_compl_inf_tol", C.c_double),
         ("acceptable_obj_change_tol", C.c_double), ("kappa_soc", C.c_double),
         ("soft_resto_pderror_reduction_factor", C.c_double), ("obj_max_inc", C.c_double),
-        ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
+        ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double), ("dual_inf_tol", C.c_double),
+        ("constr_viol_tol", C.c_double), ("compl_inf_tol", C.c_double),
         ("acceptable_iter", C.c_int32), ("max_soc", C.c_int32), ("watchdog_shortened_iter_trigger", C.c_int32),
         ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32),
-        ("max_filter_resets", C.c_int32), ("filter_reset_trigger", C.c_int32), ("reserved", C.c_int32),
+        ("max_filter_resets", C.c_int32), ("filter_reset_trigger", C.c_int32), ("precision", C.c_int32),
     ]
 
 
@@ -66,6 +67,7 @@ SIGNATURES = {
     "mpcg_track_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_synchronize": ([C.c_void_p], C.c_int),
+    "mpcg_solve_multi": ([C.c_int, C.POINTER(C.c_int), _PP, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip], C.c_int),
     "mpcg_set_strategy": ([C.c_void_p, C.c_int32], C.c_int),
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
 }

@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmpcg.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpc_planner.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpcg_multi.cpp",
+                                           "mpc_planner.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h")] + [
     os.path.join(ROOT, "include", f) for f in ("mpcg.h", "mpc_planner.h")]
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
@@ -60,7 +61,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
            f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"']
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
-    cmd += SOURCES + ["-o", LIB + ".tmp"]
+    cmd += SOURCES + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

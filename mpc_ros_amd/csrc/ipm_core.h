@@ -69,7 +69,11 @@ struct IpmParams {
     int filter_reset_trigger;           // 5
     double tiny_step_tol;               // 10 eps
     double tiny_step_y_tol;             // 1e-2
+    double dual_inf_tol;                // 1
+    double constr_viol_tol;             // 1e-4
+    double compl_inf_tol;               // 1e-4
     int cpu_iter_budget;                // max_cpu_time as iterations (-1 = none): status UNKNOWN beyond
+    int precision;                      // 0: fp64 (Ipopt's); 1: fp32 solver (differential drive)
 };
 
 // Status numbering of CppAD::ipopt::solve_result::status_type
@@ -148,12 +152,18 @@ void sincos_large(double a, double* s, double* c) {
 #endif
 }
 
-template <typename T>
-MPCG_HD void sc_t(T a, T* s, T* c) {
+MPCG_HD void sc_t(double a, double* s, double* c) {
     if (__builtin_expect(fabs(a) < 823549.6, 1))
         sincos_small(a, s, c);
     else
         sincos_large(a, s, c);  // out of line: never reached by a bounded trajectory
+}
+// fp32 solver: the same kernel in double, rounded once
+MPCG_HD void sc_t(float a, float* s, float* c) {
+    double sd, cd;
+    sc_t((double)a, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
 }
 
 // max / min with C fmax / fmin (IEEE maxNum) semantics, as the oracle: one v_max_f64 /
@@ -175,6 +185,14 @@ MPCG_HD double rcp(double x) {
     return __builtin_fma(r, e, r);
 #else
     return 1.0 / x;
+#endif
+}
+MPCG_HD float rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
+#else
+    return 1.0f / x;
 #endif
 }
 

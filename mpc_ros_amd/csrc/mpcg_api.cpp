@@ -81,6 +81,9 @@ static void ipopt_defaults(mpcg_params* p) {
     p->obj_max_inc = 5.0;
     p->tiny_step_tol = 10.0 * 2.220446049250313e-16;
     p->tiny_step_y_tol = 1e-2;
+    p->dual_inf_tol = 1.0;
+    p->constr_viol_tol = 1e-4;
+    p->compl_inf_tol = 1e-4;
     p->acceptable_iter = 15;
     p->max_soc = 4;
     p->watchdog_shortened_iter_trigger = 10;
@@ -182,7 +185,8 @@ int mpcg_params_check(const mpcg_params* p) {
         p->watchdog_trial_iter_max < 0 || p->max_soft_resto_iters < 0 || p->max_filter_resets < 0 ||
         p->filter_reset_trigger < 1)
         return fail(-1, "invalid Ipopt integer option");
-    if (!(p->soft_resto_pderror_reduction_factor >= 0) || !(p->tiny_step_tol >= 0) || !(p->kappa_soc > 0))
+    if (!(p->soft_resto_pderror_reduction_factor >= 0) || !(p->tiny_step_tol >= 0) || !(p->kappa_soc > 0) ||
+        !(p->dual_inf_tol > 0) || !(p->constr_viol_tol > 0) || !(p->compl_inf_tol > 0))
         return fail(-1, "invalid Ipopt option");
     if (!(p->dt > 0) || !std::isfinite(p->dt)) return fail(-1, "DT must be > 0");
     if (!(p->max_angvel > 0) || !(p->max_throttle > 0) || !(p->bound > 0)) return fail(-1, "bounds must be > 0");
@@ -195,6 +199,8 @@ int mpcg_params_check(const mpcg_params* p) {
     if (!(p->bound_relax_factor >= 0) || !(p->mu_init > 0)) return fail(-1, "invalid Ipopt options");
     if (p->model != 0 && p->model != 1) return fail(-1, "model must be 0 (differential drive) or 1 (bicycle)");
     if (p->model == 1 && !(p->wheelbase > 0)) return fail(-1, "model 1 needs wheelbase (LF) > 0");
+    if (p->precision != 0 && p->precision != 1) return fail(-1, "precision must be 0 (fp64) or 1 (fp32)");
+    if (p->precision == 1 && p->model != 0) return fail(-1, "precision 1 (fp32) runs the differential drive only");
     return 0;
 }
 
@@ -239,7 +245,11 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
     q.filter_reset_trigger = p.filter_reset_trigger;
     q.tiny_step_tol = p.tiny_step_tol;
     q.tiny_step_y_tol = p.tiny_step_y_tol;
+    q.dual_inf_tol = p.dual_inf_tol;
+    q.constr_viol_tol = p.constr_viol_tol;
+    q.compl_inf_tol = p.compl_inf_tol;
     q.cpu_iter_budget = cpu_iter_budget(p.max_cpu_time, p.steps);
+    q.precision = p.precision;
     return q;
 }
 
@@ -413,7 +423,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
         if (e != hipSuccess) return hip_fail(e, "solve-order sort");
         order = ord;
     }
-    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, h->d_spill, s);
+    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, (void*)h->d_spill, s);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     return record_on(h, s);
 }

@@ -16,7 +16,7 @@ size_t wide_lds_bytes(const IpmParams& P);
 size_t wide_spill_bytes(const IpmParams& P, int64_t B);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             double* spill, hipStream_t stream);
+                             void* spill, hipStream_t stream);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the
 // launch that writes the workgroup -> problem map into `buf` (returned in *order).
 size_t wide_sched_bytes(int64_t B);

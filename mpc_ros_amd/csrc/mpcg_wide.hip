@@ -24,41 +24,43 @@ struct WideArgs {
     int32_t* status;
     double* obj;
     int32_t* iters;
-    double* spill;         // per-problem HBM spill areas (WideLayout::spill() doubles each)
+    void* spill;           // per-problem HBM spill areas (WideLayout::spill() elements of T each)
 };
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
 // budget of 256 per lane lets all of them be resident
 // SPLIT (N <= 32): the recursions and the step statistics use both half-waves (wide_core.h)
-template <int MODEL, bool SPLIT>
+// T: the solver's arithmetic type (double; float for precision 1).  Inputs and outputs
+// stay double at the boundary.
+template <int MODEL, bool SPLIT, class T>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
     const int t = threadIdx.x;
-    IpmProblem<double> pr;
+    IpmProblem<T> pr;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) pr.init[j] = a.state[p * 6 + j];
+    for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pr.c[j] = a.coeffs[p * 4 + j];
+    for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
     DevWave wv;
     wv.t = t;
     const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
-    WideSolver<DevWave, MODEL, SPLIT> S(a.P, pr, wv, a.spill + p * (int64_t)Lw.spill());
+    WideSolver<DevWave, MODEL, SPLIT, T> S(a.P, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
     S.solve();
-    const double o = S.objective_out();
+    const double o = (double)S.objective_out();
     const int N = a.P.N;
     if (t == 0) {
-        a.u0[p * 2 + 0] = S.x_ctrl(0, 0);
-        a.u0[p * 2 + 1] = S.x_ctrl(1, 0);
+        a.u0[p * 2 + 0] = (double)S.x_ctrl(0, 0);
+        a.u0[p * 2 + 1] = (double)S.x_ctrl(1, 0);
         if (a.status) a.status[p] = S.status;
         if (a.iters) a.iters[p] = S.iter;
         if (a.obj) a.obj[p] = o;
     }
     if (a.traj && t < N) {
         double* tr = a.traj + p * 3 * N;
-        tr[t] = S.x_state(0, t);
-        tr[N + t] = S.x_state(1, t);
-        tr[2 * N + t] = S.x_state(2, t);
+        tr[t] = (double)S.x_state(0, t);
+        tr[N + t] = (double)S.x_state(1, t);
+        tr[2 * N + t] = (double)S.x_state(2, t);
     }
 }
 
@@ -100,20 +102,26 @@ hipError_t launch_wide_order(int64_t B, const double* coeffs, void* buf, size_t 
     return e;
 }
 
-size_t wide_lds_bytes(const IpmParams& P) { return (size_t)WideLayout(P.N, P.filter_cap, P.model).total() * sizeof(double); }
+static size_t elem_bytes(const IpmParams& P) { return P.precision == 1 ? sizeof(float) : sizeof(double); }
+size_t wide_lds_bytes(const IpmParams& P) {
+    return (size_t)WideLayout(P.N, P.filter_cap, P.model).total() * elem_bytes(P);
+}
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
-    return (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * sizeof(double) * (size_t)B;
+    return (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)B;
 }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             double* spill, hipStream_t stream) {
+                             void* spill, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
     const bool split = P.N <= 32;
-    const void* fn = P.model == 1 ? (split ? (const void*)k_solve_wide<1, true> : (const void*)k_solve_wide<1, false>)
-                                  : (split ? (const void*)k_solve_wide<0, true> : (const void*)k_solve_wide<0, false>);
+    const bool f32 = P.precision == 1;
+    if (f32 && P.model != 0) return hipErrorInvalidValue;  // (fp32: the differential drive)
+    const void* fn = f32 ? (split ? (const void*)k_solve_wide<0, true, float> : (const void*)k_solve_wide<0, false, float>)
+                   : P.model == 1 ? (split ? (const void*)k_solve_wide<1, true, double> : (const void*)k_solve_wide<1, false, double>)
+                                  : (split ? (const void*)k_solve_wide<0, true, double> : (const void*)k_solve_wide<0, false, double>);
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -122,14 +130,18 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, spill};
-    if (P.model == 1 && split)
-        hipLaunchKernelGGL((k_solve_wide<1, true>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    if (f32 && split)
+        hipLaunchKernelGGL((k_solve_wide<0, true, float>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    else if (f32)
+        hipLaunchKernelGGL((k_solve_wide<0, false, float>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    else if (P.model == 1 && split)
+        hipLaunchKernelGGL((k_solve_wide<1, true, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
     else if (P.model == 1)
-        hipLaunchKernelGGL((k_solve_wide<1, false>), dim3((unsigned)B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((k_solve_wide<1, false, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
     else if (split)
-        hipLaunchKernelGGL((k_solve_wide<0, true>), dim3((unsigned)B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((k_solve_wide<0, true, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
     else
-        hipLaunchKernelGGL((k_solve_wide<0, false>), dim3((unsigned)B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((k_solve_wide<0, false, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -47,6 +47,9 @@ struct DevWaveBase {
     typedef MPCG_LDS double2 ldsT2;
     int t;
     __device__ __forceinline__ static ldsT* S() { return (ldsT*)(__SIZE_TYPE__)0; }
+    // the LDS base as an array of U (double: the fp64 solver; float: the fp32 solver)
+    template <class U>
+    __device__ __forceinline__ static MPCG_LDS U* Sp() { return (MPCG_LDS U*)(__SIZE_TYPE__)0; }
 
     __device__ __forceinline__ void sync() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -60,6 +63,52 @@ struct DevWaveBase {
     }
     __device__ __forceinline__ void st2(int i, double a, double b) const {
         *(ldsT2*)(S() + i) = double2{a, b};
+    }
+    // (fp32 solver: 8-byte pair loads)
+    __device__ __forceinline__ void ld2(int i, float& a, float& b) const {
+        const float2 v = *(const MPCG_LDS float2*)(Sp<float>() + i);
+        a = v.x;
+        b = v.y;
+    }
+    template <int pat>
+    __device__ __forceinline__ static float swz(float v) {
+        return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), pat));
+    }
+    template <int ctrl>
+    __device__ __forceinline__ static float dpp(float v) {
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+    }
+    template <int s>
+    __device__ __forceinline__ float rpart(float v) const {
+        if (s == 0) return dpp<0xB1>(v);
+        if (s == 1) return dpp<0x4E>(v);
+        if (s == 2) return dpp<0x141>(v);
+        if (s == 3) return dpp<0x140>(v);
+        if (s == 4) return swz<0x1F | (0x10 << 10)>(v);
+        return __shfl_xor(v, 32, 64);
+    }
+    __device__ __forceinline__ float up1(float v) const { return dpp<0x138>(v); }
+    __device__ __forceinline__ float dn1(float v) const { return dpp<0x130>(v); }
+    template <bool UP, int n>
+    __device__ __forceinline__ static void shift(float* x, const float* y) {
+#pragma unroll
+        for (int q = 0; q < n; ++q)
+            x[q] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x[q]), __float_as_int(y[q]),
+                                                              UP ? 0x138 : 0x130, 0xF, 0xF, false));
+    }
+    __device__ __forceinline__ void up8(float* x, const float* y) const { shift<true, 8>(x, y); }
+    __device__ __forceinline__ void dn6(float* x, const float* y) const { shift<false, 6>(x, y); }
+    __device__ __forceinline__ float lo_half(float v) const {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+        return __int_as_float((int)r[0]);
+    }
+    __device__ __forceinline__ void xor32_pair(float v, float& a, float& b) const {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+        a = __int_as_float((int)r[0]);
+        b = __int_as_float((int)r[1]);
+    }
+    __device__ __forceinline__ float uni_d(float v) const {
+        return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
     }
     template <int pat>
     __device__ __forceinline__ static double swz(double v) {

@@ -98,9 +98,13 @@ struct WideLayout {
 // SPLIT (N <= 32): the step and multiplier recursions run in both half-waves (lane t and
 // t + 32 hold stage t & 31), and the step statistics take the stage's variables 0..3 in
 // the lower and 4..7 in the upper half-wave: half the per-variable work per lane.
-template <class WV, int MODEL = 0, bool SPLIT = false>
+// TT: the arithmetic type -- double (Ipopt's), or float (the fp32 solver of BASELINE
+// configs[2]: every lane value, LDS array and uniform scalar in fp32; the caller states a
+// tolerance a float iterate can meet).
+template <class WV, int MODEL = 0, bool SPLIT = false, class TT = double>
 struct WideSolver {
-    typedef double T;
+    typedef TT T;
+    static constexpr double EPS = sizeof(TT) == 4 ? 1.1920928955078125e-07 : 2.220446049250313e-16;
     const IpmParams P;
     const IpmProblem<T> pr;
     WV wv;
@@ -124,7 +128,7 @@ struct WideSolver {
     // OptimalityErrorConvergenceCheck)
     int in_wd, wd_short, wd_trial_iter, tiny_last, tiny_flag, in_soft, soft_count, acc_counter, have_acc;
 
-    double* spill;  // this problem's HBM spill area (WideLayout::spill() doubles)
+    T* spill;  // this problem's HBM spill area (WideLayout::spill() elements)
     // Rarely used wave-uniform solver state lives in the problem's LDS control block
     // (registers are the scarcer resource: every scalar held across the iteration loop
     // competes with the sweeps).  x() = v stores (lane 0), x() reads (uniform).
@@ -170,7 +174,7 @@ struct WideSolver {
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
-    MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_, double* spill_)
+    MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_, T* spill_)
         : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf),
           spill(spill_) {}
 
@@ -197,12 +201,12 @@ struct WideSolver {
     }
 
     // ------------------------------------------------------------ LDS helpers
-    MPCG_HD T ld(int i) const { return wv.S()[i]; }
-    MPCG_HD void st(int i, T v) const { wv.S()[i] = v; }
+    MPCG_HD T ld(int i) const { return wv.template Sp<T>()[i]; }
+    MPCG_HD void st(int i, T v) const { wv.template Sp<T>()[i] = v; }
     template <int n>
     MPCG_HD void ldn(int i, T* v) const {
 #pragma unroll
-        for (int j = 0; j < n; ++j) v[j] = wv.S()[i + j];
+        for (int j = 0; j < n; ++j) v[j] = wv.template Sp<T>()[i + j];
     }
 
     // ------------------------------------------------------ wave reductions
@@ -319,13 +323,13 @@ struct WideSolver {
         for (int j = 0; j < 6; ++j) rs[j] = m[j] > (T)100 ? (T)100 / m[j] : (T)1;
     }
     MPCG_HD void bounds_only() {
-        const T rl = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.bound));
+        const T rl = (T)fmin(P.constr_viol_tol, P.bound_relax_factor * fmax(1.0, P.bound));
         // (uniform values made scalar: the register allocator keeps them in SGPRs rather
         // than spilling vector copies to scratch)
         sl0 = wv.uni_d((T)-P.bound); su0 = wv.uni_d((T)P.bound); sl = wv.uni_d(sl0 - rl); su = wv.uni_d(su0 + rl);
-        const T rw = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_w));
+        const T rw = (T)fmin(P.constr_viol_tol, P.bound_relax_factor * fmax(1.0, P.max_w));
         wl0 = wv.uni_d((T)-P.max_w); wu0 = wv.uni_d((T)P.max_w); wl = wv.uni_d(wl0 - rw); wu = wv.uni_d(wu0 + rw);
-        const T rA = (T)fmin(1e-4, P.bound_relax_factor * fmax(1.0, P.max_a));
+        const T rA = (T)fmin(P.constr_viol_tol, P.bound_relax_factor * fmax(1.0, P.max_a));
         al0 = wv.uni_d((T)-P.max_a); au0 = wv.uni_d((T)P.max_a); al = wv.uni_d(al0 - rA); au = wv.uni_d(au0 + rA);
     }
     MPCG_HD void setup() {
@@ -1027,7 +1031,7 @@ struct WideSolver {
             const T Rt01 = tw * (m26 + m56) + m66;
             const T Rt11 = qd7 + (dt * m36 + m76);
             const T det = Rt00 * Rt11 - Rt01 * Rt01;
-            bad = bad || !(Rt00 > 0) || !(det > (T)1e-14 * Rt00 * Rt11);
+            bad = bad || !(Rt00 > 0) || !(det > (T)(sizeof(T) == 4 ? 1e-6 : 1e-14) * Rt00 * Rt11);
             const T rt0 = qv6 + (tw * (m7[2] + m7[5]) + m7[6]);
             const T rt1 = qv7 + (dt * m7[3] + m7[7]);
             const T rdet = rcp(det);
@@ -1498,7 +1502,7 @@ struct WideSolver {
     // ------------------------------------------------------------ the filter
     // Ipopt's FilterLSAcceptor / Filter (oracle/ipm.c: set_ref .. update_for_next).
     MPCG_HD static bool compare_le(T lhs, T rhs, T bas) {  // IpUtils Compare_le
-        return lhs - rhs <= (T)(10.0 * 2.220446049250313e-16) * (T)fabs(bas);
+        return lhs - rhs <= (T)(10.0 * EPS) * (T)fabs(bas);
     }
     // the reference point of a line search; the switching-condition powers once per search
     MPCG_HD void set_ref(T th, T ph, T gd) {
@@ -1909,12 +1913,19 @@ struct WideSolver {
                                 compl_uns <= (T)P.acceptable_compl_inf_tol &&
                                 fabs(last_obj() - curr_obj()) / tmax((T)1, (T)fabs(curr_obj())) <=
                                     (T)P.acceptable_obj_change_tol);
+#ifdef MPCG_TRACE
+        if (wv.lane() == 0)
+            printf("it %d mu %.3e E0 %.3e dual %.3e prim %.3e compl %.3e duns %.3e puns %.3e cuns %.3e th %.3e\n", iter,
+                   (double)mu, (double)E0, (double)(dual_inf / sd), (double)prim_inf, (double)(compl0 / scc),
+                   (double)dual_uns, (double)prim_uns, (double)compl_uns, (double)theta);
+#endif
         int s = 0;
         // Ipopt's invalid-number test on f and g at the iterate (the max-norms above
         // drop a NaN; the sums do not)
         if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval)) {
             s = IPM_INVALID_NUMBER;
-        } else if (E0 <= (T)P.tol && dual_uns <= (T)1 && prim_uns <= (T)1e-4 && compl_uns <= (T)1e-4) {
+        } else if (E0 <= (T)P.tol && dual_uns <= (T)P.dual_inf_tol && prim_uns <= (T)P.constr_viol_tol &&
+                   compl_uns <= (T)P.compl_inf_tol) {
             s = IPM_SUCCESS;
         } else {
             if (P.acceptable_iter > 0 && cur_acceptable) {
@@ -1928,7 +1939,7 @@ struct WideSolver {
         s = wv.uni(s);
         if (s) return s;
         const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
-        const T mu_min = (T)(fmin(P.tol, 1e-4) / 11.0);  // min(tol, compl_inf_tol) / (kappa_eps + 1)
+        const T mu_min = (T)(fmin(P.tol, P.compl_inf_tol) / 11.0);  // min(tol, compl_inf_tol) / (kappa_eps + 1)
         int tf = tiny_flag;
         tiny_flag = 0;
         bool done = false;
@@ -1969,7 +1980,7 @@ struct WideSolver {
             else
                 delta_w = (dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
             ++inertia_attempt;
-            if (wv.uni(delta_w > (T)1e40)) return IPM_ERROR_IN_STEP;
+            if (wv.uni((double)delta_w > 1e40 || !isfinite((double)delta_w))) return IPM_ERROR_IN_STEP;
             return do_solve(0, delta_w, K_NEWTON);
         }
         if (sv_delta > 0) dw_last = sv_delta;

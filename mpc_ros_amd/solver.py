@@ -16,10 +16,24 @@ from .params import PLUGIN_DEFAULTS
 # Ipopt options of the reference's solve (mpc_planner.cpp:356-368: max_cpu_time 0.5, the
 # rest Ipopt 3.12 defaults); any mpcg_params field can be overridden by keyword
 IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor=1e-8, mu_init=0.1, max_cpu_time=0.5)
+# the fp32 solver (precision 1, BASELINE configs[2]): tolerances a float iterate can meet --
+# the scaled dual infeasibility of an fp32 iterate stalls near 1e-4 (multipliers ~1e3 times
+# FLT_EPSILON) and mu_min = min(tol, compl_inf_tol) / 11 must stay above float resolution
+# Near the solution an fp32 iterate often cannot certify convergence (its dual residual
+# stalls): acceptable termination at 1e-3 and a 300-iteration cap end such stalls (measured
+# on the infinity set: the controls of those problems equal the fp64 solution to ~1e-5).
+FP32_OPTIONS = dict(precision=1, tol=2e-4, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
+                    acceptable_tol=1e-3, max_iter=300)
 
 
 class BatchSolver:
-    def __init__(self, device: int = 0, params: dict | None = None, strategy: str = "wave", **ipopt):
+    def __init__(self, device: int = 0, params: dict | None = None, strategy: str = "wave", dtype: str = "fp64",
+                 **ipopt):
+        """dtype "fp32": the fp32 solver with FP32_OPTIONS (overridable by keyword)."""
+        if dtype == "fp32":
+            ipopt = dict(FP32_OPTIONS, **ipopt)
+        elif dtype != "fp64":
+            raise ValueError("dtype must be 'fp64' or 'fp32'")
         L = _lib.lib()
         h = C.c_void_p()
         _lib.check(L.mpcg_create(int(device), C.byref(h)), "mpcg_create")
@@ -141,3 +155,33 @@ class BatchSolver:
         _lib.check(_lib.lib().mpcg_track_device(
             self._h, B, M, ptr(pose), ptr(vel), ptr(plan), int(bool(delay_mode)), ptr(cmd), ptr(traj), ptr(status),
             C.c_void_p(stream.cuda_stream)), "mpcg_track_device")
+
+
+def solve_multi(devices, params: dict | None = None, state=None, coeffs=None, dtype: str = "fp64", **ipopt) -> dict:
+    """mpcg_solve_multi: one process, the batch sharded over `devices`, results gathered to
+    devices[0] by RCCL (include/mpcg.h)."""
+    state = np.ascontiguousarray(state, dtype=np.float64)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    B = state.shape[0]
+    assert state.shape == (B, 6) and coeffs.shape == (B, 4), "state [B,6], coeffs [B,4]"
+    if dtype == "fp32":
+        ipopt = dict(FP32_OPTIONS, **ipopt)
+    p = _lib.params_from_map(params if params is not None else PLUGIN_DEFAULTS)
+    opts = dict(IPOPT_DEFAULTS)
+    opts.update(ipopt)
+    for k, v in opts.items():
+        setattr(p, k, v)
+    N = p.steps
+    u0 = np.zeros((B, 2))
+    traj = np.zeros((B, 3, N))
+    status = np.zeros(B, dtype=np.int32)
+    iters = np.zeros(B, dtype=np.int32)
+    obj = np.zeros(B)
+    dev = (C.c_int * len(devices))(*devices)
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int32)
+    _lib.check(_lib.lib().mpcg_solve_multi(
+        len(devices), dev, C.byref(p), B, state.ctypes.data_as(dp), coeffs.ctypes.data_as(dp), u0.ctypes.data_as(dp),
+        traj.ctypes.data_as(dp), status.ctypes.data_as(ip), obj.ctypes.data_as(dp), iters.ctypes.data_as(ip)),
+        "mpcg_solve_multi")
+    return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters)

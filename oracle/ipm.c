@@ -80,6 +80,9 @@ void ora_ipm_default_opts(ora_ipm_opts* o) {
     o->tiny_step_tol = 10.0 * EPS_MACH;
     o->tiny_step_y_tol = 1e-2;
     o->cpu_iter_budget = -1;
+    o->dual_inf_tol = 1.0;
+    o->constr_viol_tol = 1e-4;
+    o->compl_inf_tol = 1e-4;
 }
 
 int ora_cpu_iter_budget(double max_cpu_time, int steps) {
@@ -1061,7 +1064,8 @@ static int resto_convergence(ipm* S) {
     }
     if (status < 0) {
         /* the restoration problem's own optimality */
-        if (S->E0 <= o->tol && S->dual_uns <= 1.0 && S->prim_uns <= 1e-4 && S->compl_uns <= 1e-4) {
+        if (S->E0 <= o->tol && S->dual_uns <= o->dual_inf_tol && S->prim_uns <= o->constr_viol_tol &&
+            S->compl_uns <= o->compl_inf_tol) {
             O->P->cons(O->P, S->w, O->ct);
             return amax(O->m, O->ct) <= 1e2 * o->tol ? ORA_FEASIBLE_POINT_FOUND : ORA_LOCAL_INFEASIBILITY;
         }
@@ -1076,7 +1080,7 @@ static int resto_convergence(ipm* S) {
 static int ipm_iterate(ipm* S) {
     const ora_ipm_opts* o = S->o;
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
-    const double mu_min = fmin(o->tol, 1e-4) / (kappa_eps + 1.0);
+    const double mu_min = fmin(o->tol, o->compl_inf_tol) / (kappa_eps + 1.0);
     for (;;) {
         eval_current(S);
         {
@@ -1095,7 +1099,8 @@ static int ipm_iterate(ipm* S) {
             int st = resto_convergence(S);
             if (st >= 0) return st;
         } else {
-            if (S->E0 <= o->tol && S->dual_uns <= 1.0 && S->prim_uns <= 1e-4 && S->compl_uns <= 1e-4)
+            if (S->E0 <= o->tol && S->dual_uns <= o->dual_inf_tol && S->prim_uns <= o->constr_viol_tol &&
+                S->compl_uns <= o->compl_inf_tol)
                 return ORA_SUCCESS;
             if (o->acceptable_iter > 0 && current_is_acceptable(S)) {
                 if (++S->acc_counter >= o->acceptable_iter) return ORA_STOP_AT_ACCEPTABLE_POINT;
@@ -1216,8 +1221,8 @@ int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out
     for (int i = 0; i < nw; ++i) {
         P.hasL[i] = wl0[i] > -INF_BOUND;
         P.hasU[i] = wu0[i] < INF_BOUND;
-        double rl = fmin(1e-4, opts.bound_relax_factor * fmax(1.0, fabs(wl0[i])));
-        double ru = fmin(1e-4, opts.bound_relax_factor * fmax(1.0, fabs(wu0[i])));
+        double rl = fmin(opts.constr_viol_tol, opts.bound_relax_factor * fmax(1.0, fabs(wl0[i])));
+        double ru = fmin(opts.constr_viol_tol, opts.bound_relax_factor * fmax(1.0, fabs(wu0[i])));
         wl[i] = P.hasL[i] ? wl0[i] - rl : -INFINITY;
         wu[i] = P.hasU[i] ? wu0[i] + ru : INFINITY;
     }

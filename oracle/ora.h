@@ -85,6 +85,9 @@ typedef struct ora_ipm_opts {
      * budget: CPUTIME_EXCEEDED (-> solve_result unknown, solve_callback.hpp:1165-1167) once
      * iter > cpu_iter_budget; < 0 = no budget (see ora_cpu_iter_budget) */
     int cpu_iter_budget;
+    double dual_inf_tol;                /* 1 */
+    double constr_viol_tol;             /* 1e-4 */
+    double compl_inf_tol;               /* 1e-4 */
 } ora_ipm_opts;
 
 /* Result; status uses CppAD::ipopt::solve_result::status_type numbering

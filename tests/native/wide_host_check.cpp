@@ -12,6 +12,7 @@
 //         acceptable_compl_inf_tol acceptable_obj_change_tol max_soc kappa_soc wd_trigger
 //         wd_trial_max soft_factor max_soft_iters obj_max_inc max_filter_resets
 //         filter_reset_trigger tiny_step_tol tiny_step_y_tol cpu_iter_budget filter_cap
+//         dual_inf_tol constr_viol_tol compl_inf_tol
 //         B, then B x (state[6], coeffs[4])
 // stdout: per problem: status iters obj u0[2] traj[3N]
 #include <barrier>
@@ -29,12 +30,27 @@ struct HostShared {
     std::vector<double> lds;
 };
 
+#ifndef HOST_T
+#define HOST_T double  // -DHOST_T=float: the fp32 solver
+#endif
+typedef HOST_T HT;
+
 struct HostWave {
     HostShared* sh;
     int t;
     double* lds;
     double* S() const { return lds; }
+    template <class U>
+    U* Sp() const { return reinterpret_cast<U*>(lds); }
     void sync() const { sh->bar.arrive_and_wait(); }
+    template <class U>
+    U from(U v, int src) const {
+        sh->xd[t] = (double)v;
+        sync();
+        const U r = (U)sh->xd[src];
+        sync();
+        return r;
+    }
     double xor_(double v, int m) const {
         sh->xd[t] = v;
         sync();
@@ -42,10 +58,11 @@ struct HostWave {
         sync();
         return r;
     }
-    double up1(double v) const {
-        sh->xd[t] = v;
+    template <class U>
+    U up1(U v) const {
+        sh->xd[t] = (double)v;
         sync();
-        const double r = t > 0 ? sh->xd[t - 1] : v;
+        const U r = t > 0 ? (U)sh->xd[t - 1] : v;
         sync();
         return r;
     }
@@ -73,48 +90,42 @@ struct HostWave {
     int lane() const { return t; }
     void mark(int) const {}
     void sched_fence() const {}
-    void ld2(int i, double& a, double& b) const {
-        a = lds[i];
-        b = lds[i + 1];
+    template <class U>
+    void ld2(int i, U& a, U& b) const {
+        a = Sp<U>()[i];
+        b = Sp<U>()[i + 1];
     }
-    void st2(int i, double a, double b) const {
-        lds[i] = a;
-        lds[i + 1] = b;
-    }
-    double from(double v, int src) const {
-        sh->xd[t] = v;
-        sync();
-        const double r = sh->xd[src];
-        sync();
-        return r;
-    }
-    double dn1(double v) const { return from(v, t < 63 ? t + 1 : t); }
+    template <class U>
+    U dn1(U v) const { return from(v, t < 63 ? t + 1 : t); }
     // device: DPP wave_shr:1 / wave_shl:1 with bound_ctrl off (lane 0 / 63 keeps x)
-    void up8(double* x, const double* y) const {
+    template <class U>
+    void up8(U* x, const U* y) const {
         for (int q = 0; q < 8; ++q) {
-            const double r = from(y[q], t > 0 ? t - 1 : t);
+            const U r = from(y[q], t > 0 ? t - 1 : t);
             if (t > 0) x[q] = r;
         }
     }
-    void dn6(double* x, const double* y) const {
+    template <class U>
+    void dn6(U* x, const U* y) const {
         for (int q = 0; q < 6; ++q) {
-            const double r = from(y[q], t < 63 ? t + 1 : t);
+            const U r = from(y[q], t < 63 ? t + 1 : t);
             if (t < 63) x[q] = r;
         }
     }
-    double lo_half(double v) const { return from(v, t & 31); }
+    template <class U>
+    U lo_half(U v) const { return from(v, t & 31); }
     // device: v_permlane32_swap gives the lower half (own, partner), the upper (partner, own)
-    void xor32_pair(double v, double& a, double& b) const {
-        const double o = from(v, t ^ 32);
+    template <class U>
+    void xor32_pair(U v, U& a, U& b) const {
+        const U o = from(v, t ^ 32);
         a = t < 32 ? v : o;
         b = t < 32 ? o : v;
     }
-    double uni_d(double v) const { return from(v, 0); }
-    template <int q>
-    double bcast8(double v) const { return from(v, (t & ~7) | q); }
+    template <class U>
+    U uni_d(U v) const { return from(v, 0); }
     // reduction partners of the device (wave_dev.h): xor 1, xor 2, mirror 8, mirror 16, xor 16, xor 32
-    template <int s>
-    double rpart(double v) const {
+    template <int s, class U>
+    U rpart(U v) const {
         const int p = s == 0 ? t ^ 1 : s == 1 ? t ^ 2 : s == 2 ? (t & ~7) | (7 - (t & 7))
                     : s == 3 ? (t & ~15) | (15 - (t & 15)) : s == 4 ? t ^ 16 : t ^ 32;
         return from(v, p);
@@ -140,16 +151,17 @@ int main() {
                    &P.obj_max_inc, &P.max_filter_resets, &P.filter_reset_trigger, &P.tiny_step_tol,
                    &P.tiny_step_y_tol, &P.cpu_iter_budget, &P.filter_cap) != 19)
         return 1;
+    if (std::scanf("%lf %lf %lf", &P.dual_inf_tol, &P.constr_viol_tol, &P.compl_inf_tol) != 3) return 1;
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     const mpcg::WideLayout L(P.N, P.filter_cap, P.model);
     for (long b = 0; b < B; ++b) {
-        mpcg::IpmProblem<double> pr;
-        for (double& v : pr.init) std::scanf("%lf", &v);
-        for (double& v : pr.c) std::scanf("%lf", &v);
+        mpcg::IpmProblem<HT> pr;
+        for (HT& v : pr.init) { double d; std::scanf("%lf", &d); v = (HT)d; }
+        for (HT& v : pr.c) { double d; std::scanf("%lf", &d); v = (HT)d; }
         HostShared sh;
         sh.lds.assign(L.total(), std::nan(""));
-        std::vector<double> spill(L.spill(), std::nan(""));
+        std::vector<HT> spill(L.spill(), (HT)std::nan(""));
         int status = 0, iters = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
@@ -171,16 +183,16 @@ int main() {
                     }
                 };
                 if (P.model == 1 && P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 1, true> S(P, pr, wv, spill.data());
+                    mpcg::WideSolver<HostWave, 1, true, HT> S(P, pr, wv, spill.data());
                     run(S);
                 } else if (P.model == 1) {
-                    mpcg::WideSolver<HostWave, 1, false> S(P, pr, wv, spill.data());
+                    mpcg::WideSolver<HostWave, 1, false, HT> S(P, pr, wv, spill.data());
                     run(S);
                 } else if (P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 0, true> S(P, pr, wv, spill.data());
+                    mpcg::WideSolver<HostWave, 0, true, HT> S(P, pr, wv, spill.data());
                     run(S);
                 } else {
-                    mpcg::WideSolver<HostWave, 0, false> S(P, pr, wv, spill.data());
+                    mpcg::WideSolver<HostWave, 0, false, HT> S(P, pr, wv, spill.data());
                     run(S);
                 }
             });

@@ -24,7 +24,7 @@ def opts_line(o) -> str:
             f"{o.watchdog_shortened_iter_trigger} {o.watchdog_trial_iter_max} "
             f"{o.soft_resto_pderror_reduction_factor!r} {o.max_soft_resto_iters} {o.obj_max_inc!r} "
             f"{o.max_filter_resets} {o.filter_reset_trigger} {o.tiny_step_tol!r} {o.tiny_step_y_tol!r} "
-            f"{o.cpu_iter_budget} 64")
+            f"{o.cpu_iter_budget} 64\n{o.dual_inf_tol!r} {o.constr_viol_tol!r} {o.compl_inf_tol!r}")
 
 
 def run_harness(exe, P, state, coeffs, opts=None):

@@ -246,3 +246,19 @@ def test_nonfinite_inputs(torch_cuda, oracle):
     r = solver_for(P).solve(st, cf)
     check_against(r, g, min_same_iters=1.0)
     assert (g["status"] == 11).sum() == 5  # (row 2, a huge finite state: in the restoration phase)
+
+
+def test_solve_multi_one_gpu_matches_single(torch_cuda, infinity_golden):
+    """mpcg_solve_multi (one process, RCCL gather to devices[0]) on the GPUs of this box:
+    results equal the single-handle solve bitwise."""
+    import torch
+
+    from mpc_ros_amd.solver import solve_multi
+
+    g = infinity_golden
+    P = params_from_array(g["params"])
+    devs = list(range(torch.cuda.device_count()))
+    r = solve_multi(devs, P, g["state"], g["coeffs"])
+    s = solver_for(P).solve(g["state"], g["coeffs"])
+    for k in ("u0", "traj", "status", "iters", "obj"):
+        np.testing.assert_array_equal(r[k], s[k])
