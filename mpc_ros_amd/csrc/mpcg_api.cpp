@@ -348,8 +348,9 @@ static int ensure_sched(mpcg_handle* h, int64_t B) {
     return 0;
 }
 
-// 160 KiB of LDS per CU; one wavefront's problem must fit with room for a second
-static const size_t kWideLdsMax = 64 * 1024;
+// 160 KiB of LDS per CU: up to N = 64 a problem leaves room for a second wavefront (and
+// eight fit at N = 20); up to N = 128 (two stage blocks) one problem may take the CU's LDS
+static const size_t kWideLdsMax = 160 * 1024;
 
 // The handle's scratch (solve order, spill areas, track intermediates) is used
 // stream-ordered: work queued on stream s first waits for the scratch's last use on
@@ -369,7 +370,7 @@ static int record_on(mpcg_handle* h, hipStream_t s) {
     return 0;
 }
 
-static bool wave_fits(const mpcg::IpmParams& P) { return P.N <= 64 && mpcg::wide_lds_bytes(P) <= kWideLdsMax; }
+static bool wave_fits(const mpcg::IpmParams& P) { return P.N <= 128 && mpcg::wide_lds_bytes(P) <= kWideLdsMax; }
 
 int mpcg_reserve(mpcg_handle* h, int64_t B) {
     if (!h) return fail(-1, "null handle");
@@ -405,7 +406,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
     const mpcg::IpmParams P = to_ipm(h->params);
-    if (!wave_fits(P)) return fail(-1, "STEPS must be <= 64 (the problem state must fit 64 KiB of LDS)");
+    if (!wave_fits(P)) return fail(-1, "STEPS must be <= 128 (the problem state must fit the CU's 160 KiB of LDS)");
     rc = ensure_spill(h, B);
     if (rc) return rc;
     if (B > kOrderMinBatch) {

@@ -32,7 +32,8 @@ struct WideArgs {
 // SPLIT (N <= 32): the recursions and the step statistics use both half-waves (wide_core.h)
 // T: the solver's arithmetic type (double; float for precision 1).  Inputs and outputs
 // stay double at the boundary.
-template <int MODEL, bool SPLIT, class T>
+// NB: stage blocks (2 for 64 < N <= 128, lane t owning stages t and 64 + t).
+template <int MODEL, bool SPLIT, class T, int NB>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
@@ -45,7 +46,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     DevWave wv;
     wv.t = t;
     const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
-    WideSolver<DevWave, MODEL, SPLIT, T> S(a.P, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
+    WideSolver<DevWave, MODEL, SPLIT, T, NB> S(a.P, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
     S.solve();
     const double o = (double)S.objective_out();
     const int N = a.P.N;
@@ -56,11 +57,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (a.iters) a.iters[p] = S.iter;
         if (a.obj) a.obj[p] = o;
     }
-    if (a.traj && t < N) {
+    if (a.traj) {
         double* tr = a.traj + p * 3 * N;
-        tr[t] = (double)S.x_state(0, t);
-        tr[N + t] = (double)S.x_state(1, t);
-        tr[2 * N + t] = (double)S.x_state(2, t);
+        for (int k = t; k < N; k += 64) {
+            tr[k] = (double)S.x_state(0, k);
+            tr[N + k] = (double)S.x_state(1, k);
+            tr[2 * N + k] = (double)S.x_state(2, k);
+        }
     }
 }
 
@@ -118,10 +121,20 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     const size_t lds = wide_lds_bytes(P);
     const bool split = P.N <= 32;
     const bool f32 = P.precision == 1;
+    const int nb = P.N > 64 ? 2 : 1;
+    if (P.N > 128) return hipErrorInvalidValue;
     if (f32 && P.model != 0) return hipErrorInvalidValue;  // (fp32: the differential drive)
-    const void* fn = f32 ? (split ? (const void*)k_solve_wide<0, true, float> : (const void*)k_solve_wide<0, false, float>)
-                   : P.model == 1 ? (split ? (const void*)k_solve_wide<1, true, double> : (const void*)k_solve_wide<1, false, double>)
-                                  : (split ? (const void*)k_solve_wide<0, true, double> : (const void*)k_solve_wide<0, false, double>);
+    // (model, split, precision, blocks) -> instantiation
+    const void* fn;
+    if (f32)
+        fn = nb == 2 ? (const void*)k_solve_wide<0, false, float, 2>
+           : split ? (const void*)k_solve_wide<0, true, float, 1> : (const void*)k_solve_wide<0, false, float, 1>;
+    else if (P.model == 1)
+        fn = nb == 2 ? (const void*)k_solve_wide<1, false, double, 2>
+           : split ? (const void*)k_solve_wide<1, true, double, 1> : (const void*)k_solve_wide<1, false, double, 1>;
+    else
+        fn = nb == 2 ? (const void*)k_solve_wide<0, false, double, 2>
+           : split ? (const void*)k_solve_wide<0, true, double, 1> : (const void*)k_solve_wide<0, false, double, 1>;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -130,18 +143,9 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, spill};
-    if (f32 && split)
-        hipLaunchKernelGGL((k_solve_wide<0, true, float>), dim3((unsigned)B), dim3(64), lds, stream, a);
-    else if (f32)
-        hipLaunchKernelGGL((k_solve_wide<0, false, float>), dim3((unsigned)B), dim3(64), lds, stream, a);
-    else if (P.model == 1 && split)
-        hipLaunchKernelGGL((k_solve_wide<1, true, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
-    else if (P.model == 1)
-        hipLaunchKernelGGL((k_solve_wide<1, false, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
-    else if (split)
-        hipLaunchKernelGGL((k_solve_wide<0, true, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
-    else
-        hipLaunchKernelGGL((k_solve_wide<0, false, double>), dim3((unsigned)B), dim3(64), lds, stream, a);
+    void* args[] = {(void*)&a};
+    e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

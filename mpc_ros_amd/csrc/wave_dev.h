@@ -173,6 +173,21 @@ struct DevWaveBase {
         b = __hiloint2double((int)hi[1], (int)lo[1]);
     }
     __device__ __forceinline__ bool any(bool b) const { return __any(b); }
+    // the value of lane 63 / lane 0 (wave-uniform; the two-block recursions)
+    __device__ __forceinline__ double lane63(double v) const {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                                __builtin_amdgcn_readlane(__double2loint(v), 63));
+    }
+    __device__ __forceinline__ double lane0(double v) const {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 0),
+                                __builtin_amdgcn_readlane(__double2loint(v), 0));
+    }
+    __device__ __forceinline__ float lane63(float v) const {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    }
+    __device__ __forceinline__ float lane0(float v) const {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    }
     // number of lanes below this one with b set, and (total) the count over the wavefront
     __device__ __forceinline__ int ballot_prefix(bool b, int* total) const {
         const unsigned long long m = __ballot(b);

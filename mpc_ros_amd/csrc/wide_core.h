@@ -101,8 +101,12 @@ struct WideLayout {
 // TT: the arithmetic type -- double (Ipopt's), or float (the fp32 solver of BASELINE
 // configs[2]: every lane value, LDS array and uniform scalar in fp32; the caller states a
 // tolerance a float iterate can meet).
-template <class WV, int MODEL = 0, bool SPLIT = false, class TT = double>
+// NB: stage blocks -- 1 for N <= 64 (lane t owns stage t), 2 for 64 < N <= 128 (lane t owns
+// stages t and 64 + t: the stage-parallel sweeps loop over the blocks, the dynamics of
+// stage 63 reach stage 64 by a lane read, the systolic recursions run block by block).
+template <class WV, int MODEL = 0, bool SPLIT = false, class TT = double, int NB = 1>
 struct WideSolver {
+    static_assert(NB == 1 || !SPLIT, "the half-wave split is for N <= 32");
     typedef TT T;
     static constexpr double EPS = sizeof(TT) == 4 ? 1.1920928955078125e-07 : 2.220446049250313e-16;
     const IpmParams P;
@@ -365,8 +369,9 @@ struct WideSolver {
         return v;
     }
     MPCG_HD void init_point() {
-        if (t < N) {
-            const int k = t;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
             // constant entries of the stage table (dt, 0, 1, -1: gather targets of the
             // Riccati's per-lane offsets), written once
             const int sb = L.ST(k);
@@ -620,6 +625,10 @@ struct WideSolver {
             stats_split(acc, alpha, amax_z);
             return;
         }
+        if constexpr (NB == 2) {
+            stats_blk(acc, alpha, amax_z);
+            return;
+        }
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         accept_all(t, acc, alpha, amax_z);
         T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
@@ -743,6 +752,220 @@ struct WideSolver {
         wv.mark(0);
     }
 
+
+    // ------------------------------------------------------- two stage blocks (N > 64)
+    // The statistics sweep of stats() for lane t's stages t and 64 + t: stage data and
+    // F(s_k, u_k) of both blocks first, then the shift of F to stage k + 1 (stage 63 ->
+    // 64 by a lane read), then the statistics (the lane's values reloaded from LDS).
+    MPCG_HD void stats_blk(bool acc, T alpha, T amax_z) {
+        const int t = wv.lane();
+        accept_all(t, acc, alpha, amax_z);
+        T f = 0, th = 0, pinf = 0, puns = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0,
+          lg = 0;
+        T Fk[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) Fk[b][j] = 0;
+            if (k < N) {
+                const bool last = k == N - 1;
+                T w[8], yn[6] = {0, 0, 0, 0, 0, 0}, a[7] = {0, 0, 0, 0, 0, 0, 0}, cvk[5] = {0, 0, 0, 0, 0};
+                T twk = dt, tvk = 0, hvdk = 0;
+                ldn<8>(L.W(k), w);
+                if (!last) {
+                    ldn<6>(L.Y(k + 1), yn);
+                    Lin<T> ln;
+                    ln.eval(pr.c, w);
+                    ln.jac(w, dt, a);
+                    next_m(ln, w, w + 6, Fk[b]);
+                    turn_d(w, w + 6, &twk, &tvk);
+                    if (model == 1) hvdk = -(yn[2] + yn[5]) / lf * dt;
+                    const T v = w[3];
+                    cvk[0] = -yn[4] * ln.f2;
+                    cvk[1] = yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;
+                    cvk[2] = yn[0] * ln.st * dt - yn[1] * ln.ct * dt;
+                    cvk[3] = yn[4] * v * ln.se * dt;
+                    cvk[4] = -yn[4] * ln.ce * dt;
+                }
+                const int sb = L.ST(k);
+#pragma unroll
+                for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+                if (!last) {
+                    T wn[6];
+                    ldn<6>(L.W(k + 1), wn);
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) st(sb + WideLayout::SD + j, Fk[b][j] - wn[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cvk[j]);
+                if constexpr (MODEL == 1) {
+                    st(sb + WideLayout::STW, twk);
+                    st(sb + WideLayout::STV, tvk);
+                    st(sb + WideLayout::SHVD, hvdk);
+                }
+            }
+        }
+        T Fprev[NB][6];
+        shift_blocks(Fk, Fprev);
+        wv.sync();
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[8];
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            ldn<7>(L.ST(k) + WideLayout::SA, a);
+            T twk = dt, tvk = 0;
+            if constexpr (MODEL == 1) {
+                twk = ld(L.ST(k) + WideLayout::STW);
+                tvk = ld(L.ST(k) + WideLayout::STV);
+            }
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                up[0] = ld(L.W(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7);
+            }
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[b][j];
+                if (k == 0) st(L.C0() + j, -c);
+                const T rsc = rowscale(j, k);
+                const T cs = rsc * c;
+                th += fabs(cs);
+                pinf = tmax(pinf, (T)fabs(cs));
+                puns = tmax(puns, (T)fabs(c));
+                ly += fabs(y[j]) * rcp(rsc);
+            }
+            f += cost_state(w);
+            T g[6], at[6] = {0, 0, 0, 0, 0, 0}, gu[2] = {0, 0};
+            grad_state(w, g);
+            if (!last) {
+                AT_mul(a, yn, at);
+                if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
+                grad_ctrl(k, um, w + 6, up, gu);
+                f += cost_ctrl(k, w + 6, up);
+            }
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T gj = j < 6 ? sf * g[j] + y[j] - at[j] : sf * gu[j - 6] - (j == 6 ? btw : bta);
+                    const T rd = gj - zl[j] + zu[j];
+                    dinf = tmax(dinf, (T)fabs(rd));
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    slackprod *= dl * du;
+                    const T p1 = dl * zl[j], p2 = du * zu[j];
+                    c0 = tmax(c0, tmax((T)fabs(p1), (T)fabs(p2)));
+                    mn = tmin(mn, tmin(p1, p2));
+                    mx = tmax(mx, tmax(p1, p2));
+                    lz += fabs(zl[j]) + fabs(zu[j]);
+                }
+            }
+            lg += log(slackprod);
+        }
+        T v[11] = {f, th, pinf, puns, dinf, c0, mn, mx, ly, lz, lg};
+        const int op[11] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM};
+        reduce<11, true>(v, op);
+        fval = v[0];
+        theta = v[1];
+        prim_inf = v[2];
+        prim_uns = v[3];
+        dual_inf = v[4];
+        compl0 = v[5];
+        pmin = v[6];
+        pmax = v[7];
+        l1y = v[8];
+        l1z = v[9];
+        logsum = v[10];
+        wv.mark(0);
+    }
+    // F of stage k to lane k + 1 over both blocks: DPP shift within a block, lane 63 of
+    // block b - 1 to lane 0 of block b
+    MPCG_HD void shift_blocks(const T (&Fk)[NB][6], T (&Fprev)[NB][6]) const {
+        const int t = wv.lane();
+        for (int b = 0; b < NB; ++b) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                T v = wv.up1(Fk[b][j]);
+                if (b > 0) {
+                    const T c = wv.lane63(Fk[b - 1][j]);
+                    v = t == 0 ? c : v;
+                }
+                Fprev[b][j] = v;
+            }
+        }
+    }
+
+    // trial() for two stage blocks
+    MPCG_HD bool trial_blk(T alpha, T* phi, T* th) {
+        const int t = wv.lane();
+        T f = 0, thv = 0, lg = 0;
+        int bad = 0;
+        T Fk[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) Fk[b][j] = 0;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T cw[8], cd[8], w[8];
+            ldn<8>(L.W(k), cw);
+            ldn<8>(L.DW(k), cd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = cw[j] + alpha * cd[j];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    bad |= !((dl > 0) && (du > 0));
+                    slackprod *= dl * du;
+                }
+            }
+            lg += log(slackprod);
+            f += cost_state(w);
+            if (!last) {
+                T up[2];
+                up[0] = ld(L.W(k + 1) + 6) + alpha * ld(L.DW(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7) + alpha * ld(L.DW(k + 1) + 7);
+                f += cost_ctrl(k, w + 6, up);
+                Lin<T> ln;
+                ln.eval(pr.c, w);
+                next_m(ln, w, w + 6, Fk[b]);
+            }
+        }
+        T Fprev[NB][6];
+        shift_blocks(Fk, Fprev);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T wj = ld(L.W(k) + j) + alpha * ld(L.DW(k) + j);
+                const T c = k == 0 ? wj - pr.init[j] : wj - Fprev[b][j];
+                thv += fabs(rowscale(j, k) * c);
+            }
+        }
+        T v[3] = {f, thv, lg};
+        const int op[3] = {RSUM, RSUM, RSUM};
+        reduce<3, true>(v, op);
+        const bool anybad = wv.any(bad != 0);
+        wv.mark(6);
+        *phi = sf * v[0] - mu * v[2];
+        *th = v[1];
+        return !anybad && isfinite((double)*phi);
+    }
+
     // ------------------------------------------------------- Riccati backward
     // Stage data that does not depend on the cost-to-go, all stages in parallel.
     // Stage data of the Newton system (SPLIT): the lower half-wave takes the barrier
@@ -830,8 +1053,15 @@ struct WideSolver {
             return;
         }
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
-        if (t >= N) return;
-        const int k = t;
+        if constexpr (NB == 2) {
+            precompute_stage(t, mode, delta_w);
+            precompute_stage(t + 64, mode, delta_w);
+            return;
+        }
+        precompute_stage(t, mode, delta_w);
+    }
+    MPCG_HD void precompute_stage(int k, int mode, T delta_w) {
+        if (k >= N) return;
         const bool last = k == N - 1;
         const int sb = L.ST(k);
         T w[8], zl[8], zu[8];
@@ -1146,6 +1376,7 @@ struct WideSolver {
     }
 
     MPCG_HD Fwd forward(int mode) {
+        if constexpr (NB == 2) return forward_blk(mode);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         wv.sync();
         // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
@@ -1336,6 +1567,194 @@ struct WideSolver {
         return F;
     }
 
+
+    // forward() for two stage blocks: the step recursion runs over block 0 (64 stages),
+    // lane 63's output seeds lane 0 of block 1; the multiplier recursion runs over block 1,
+    // its lane 0 output seeds lane 63 of block 0 (the unmasked systolic scheme of forward()
+    // in each block).
+    MPCG_HD Fwd forward_blk(int mode) {
+        const int t = wv.lane();
+        wv.sync();
+        T xs[NB][6], dus[NB][2], xlast[8];
+        for (int b = 0; b < NB; ++b) {
+            const int ks = t + 64 * b;
+            T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
+            if (ks < N - 1) {
+                ldv<16>(L.KR(ks), K);
+                ldv<2>(L.ST(ks) + WideLayout::SKF, kf);
+                ldv<8>(L.ST(ks) + WideLayout::SA, a);
+                ldv<6>(L.ST(ks) + WideLayout::SD, d);
+                if constexpr (MODEL == 1)
+                    ld2(L.ST(ks) + WideLayout::STW, twl, tvl);
+                else
+                    twl = dt;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) K[q] = 0;
+                kf[0] = 0;
+                kf[1] = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) a[q] = 0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) d[q] = 0;
+            }
+            T x[8];
+            if (b == 0) {
+                T c0[6];
+                ldv<6>(L.C0(), c0);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) x[j] = (mode == 0 && t == 0) ? c0[j] : (T)0;
+                x[6] = 0;
+                x[7] = 0;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = t == 0 ? xlast[j] : (T)0;
+            }
+            const int steps = b == 0 ? (N < 64 ? N : 64) : N - 64;
+            T du0 = 0, du1 = 0, y[8];
+            for (int s = 0; s < steps; ++s) {
+                T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
+#pragma unroll
+                for (int m = 0; m < 8; m += 2) {
+                    u0a += K[m] * x[m];
+                    u0b += K[m + 1] * x[m + 1];
+                    u1a += K[8 + m] * x[m];
+                    u1b += K[9 + m] * x[m + 1];
+                }
+                du0 = u0a + u0b;
+                du1 = u1a + u1b;
+                A_mul(a, x, y);
+                if constexpr (MODEL == 1) {
+                    y[2] += tvl * x[3];
+                    y[5] += tvl * x[3];
+                }
+                y[2] += twl * du0;
+                y[3] += dt * du1;
+                y[5] += twl * du0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) y[j] += d[j];
+                y[6] = du0;
+                y[7] = du1;
+                wv.up8(x, y);
+            }
+            if (b == 0 && NB == 2) {
+                // lane 63 computed stage 64's input in the last step
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xlast[j] = wv.lane63(y[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) xs[b][j] = x[j];
+            dus[b][0] = du0;
+            dus[b][1] = du1;
+            if (ks < N) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) st(L.DW(ks) + j, x[j]);
+                st(L.DW(ks) + 6, du0);
+                st(L.DW(ks) + 7, du1);
+            }
+        }
+        wv.mark(3);
+        // multipliers: upper block first
+        T lam_in[6] = {0, 0, 0, 0, 0, 0};
+        for (int b = NB - 1; b >= 0; --b) {
+            const int k = t + 64 * b;
+            T base[6] = {0, 0, 0, 0, 0, 0}, ak[8], tva = 0;
+            if (k < N) {
+                T qd[8], qv[8], cv[6], hvd = 0;
+                const int sb = L.ST(k);
+                ldv<8>(sb + WideLayout::SQD, qd);
+                ldv<8>(sb + WideLayout::SQV, qv);
+                ldv<6>(sb + WideLayout::SCV, cv);
+                ldv<8>(sb + WideLayout::SA, ak);
+                if constexpr (MODEL == 1) {
+                    tva = ld(sb + WideLayout::STV);
+                    hvd = ld(sb + WideLayout::SHVD);
+                }
+                const T* x = xs[b];
+                base[0] = (qd[0] + cv[0]) * x[0] + qv[0];
+                base[1] = qd[1] * x[1] + qv[1];
+                base[2] = (qd[2] + cv[1]) * x[2] + cv[2] * x[3] + qv[2];
+                base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
+                base[4] = qd[4] * x[4] + qv[4];
+                base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
+                if constexpr (MODEL == 1) base[3] += hvd * dus[b][0];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ak[q] = 0;
+            }
+            T lam[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lam[q] = (b < NB - 1 && t == 63) ? lam_in[q] : (T)0;
+            const int steps = b == NB - 1 ? N - 64 * b : 64;
+            T o[6];
+            for (int s = steps - 1; s >= 0; --s) {
+                AT_mul(ak, lam, o);
+                if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) o[q] += base[q];
+                wv.dn6(lam, o);
+            }
+            if (k < N) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) st(L.YP(k) + q, -o[q]);
+            }
+            if (b > 0) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) lam_in[q] = wv.lane0(o[q]);
+            }
+        }
+        wv.mark(4);
+        Fwd F{(T)1, (T)1, (T)0, (T)0};
+        if (mode == 0) {
+            for (int b = 0; b < NB; ++b) {
+                const int k = t + 64 * b;
+                if (k < N) step_stats_stage(k, xs[b], dus[b], F);
+            }
+            T v[4] = {F.amax_p, F.amax_z, F.gd, F.rel};
+            const int op[4] = {RMIN, RMIN, RSUM, RMAX};
+            reduce<4, true>(v, op);
+            F.amax_p = v[0];
+            F.amax_z = v[1];
+            F.gd = v[2];
+            F.rel = v[3];
+        }
+        wv.mark(5);
+        return F;
+    }
+    // step statistics of stage k (unsplit): fraction to the boundary, grad phi^T dw, relative step
+    MPCG_HD void step_stats_stage(int k, const T* xk, const T* duk, Fwd& F) const {
+        const bool last = k == N - 1;
+        T w[8], zl[8], zu[8], dk[8];
+        ldn<8>(L.W(k), w);
+        ldn<8>(L.ZL(k), zl);
+        ldn<8>(L.ZU(k), zu);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dk[q] = xk[q];
+        dk[6] = duk[0];
+        dk[7] = duk[1];
+        T g[6], gu[2] = {0, 0};
+        grad_state(w, g);
+        if (!last) {
+            T um[2] = {0, 0}, up[2];
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            up[0] = ld(L.W(k + 1) + 6);
+            up[1] = ld(L.W(k + 1) + 7);
+            grad_ctrl(k, um, w + 6, up, gu);
+        }
+        const int nv = last ? 6 : 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j < nv) {
+                const T gj = j < 6 ? sf * g[j] : sf * gu[j - 6];
+                const T gphi = gj - mu * rcp(w[j] - vlo(j)) + mu * rcp(vhi(j) - w[j]);
+                dir_var(w[j], zl[j], zu[j], vlo(j), vhi(j), gphi, dk[j], F);
+            }
+        }
+    }
+
     // ------------------------------------------------------------ trial point
     // Trial point (SPLIT): lane k of the lower half-wave takes stage k's variables 0..3,
     // the heading theta and dynamics rows 0..3, lane 32 + k the variables 4..7, the
@@ -1426,6 +1845,7 @@ struct WideSolver {
 
     MPCG_HD bool trial(T alpha, T* phi, T* th) {
         if constexpr (SPLIT) return trial_split(alpha, phi, th);
+        if constexpr (NB == 2) return trial_blk(alpha, phi, th);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         T f = 0, thv = 0, lg = 0;
         int bad = 0;
@@ -1647,9 +2067,10 @@ struct WideSolver {
     MPCG_HD void soc_rhs(T alpha) {
         const int t = wv.lane();
         wv.sync();
+        for (int b = 0; b < NB; ++b) {
+        const int k = t + 64 * b;
         T dn[6] = {0, 0, 0, 0, 0, 0}, c0[6] = {0, 0, 0, 0, 0, 0};
-        if (t < N) {
-            const int k = t;
+        if (k < N) {
             T w[8], cw[8], cd[8];
             ldn<8>(L.W(k), cw);
             ldn<8>(L.DW(k), cd);
@@ -1671,14 +2092,15 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 6; ++j) c0[j] = -(w[j] - pr.init[j]);
         }
-        if (t < N - 1) {
-            const int sb = L.ST(t) + WideLayout::SD;
+        if (k < N - 1) {
+            const int sb = L.ST(k) + WideLayout::SD;
 #pragma unroll
             for (int j = 0; j < 6; ++j) st(sb + j, dn[j] + alpha * ld(sb + j));
         }
-        if (t == 0) {
+        if (k == 0) {
 #pragma unroll
             for (int j = 0; j < 6; ++j) st(L.C0() + j, c0[j] + alpha * ld(L.C0() + j));
+        }
         }
         wv.sync();
     }
@@ -1690,12 +2112,15 @@ struct WideSolver {
         const int t = wv.lane();
         wv.sync();
         T du = 0, pr_ = 0, cm = 0;
-        T Fk[6] = {0, 0, 0, 0, 0, 0};
-        T w[8];
-        const int k = t;
-        const bool act = t < N, last = k == N - 1;
-        if (act) {
-            T zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[7] = {0, 0, 0, 0, 0, 0, 0};
+        T Fk[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) Fk[b][j] = 0;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0},
+                a[7] = {0, 0, 0, 0, 0, 0, 0};
             T twk = dt, tvk = 0;
             ldn<8>(L.W(k), w);
             ldn<8>(L.ZL(k), zl);
@@ -1708,7 +2133,7 @@ struct WideSolver {
                 Lin<T> ln;
                 ln.eval(pr.c, w);
                 ln.jac(w, dt, a);
-                next_m(ln, w, w + 6, Fk);
+                next_m(ln, w, w + 6, Fk[b]);
                 turn_d(w, w + 6, &twk, &tvk);
             }
             if (k >= 1) {
@@ -1733,13 +2158,15 @@ struct WideSolver {
                 }
             }
         }
-        T Fprev[6];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Fprev[j] = wv.up1(Fk[j]);
-        if (act) {
+        T Fprev[NB][6];
+        shift_blocks(Fk, Fprev);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                const T wj = ld(L.W(k) + j);
+                const T c = k == 0 ? wj - pr.init[j] : wj - Fprev[b][j];
                 pr_ += fabs(rowscale(j, k) * c);
             }
         }
@@ -1770,9 +2197,12 @@ struct WideSolver {
         const int t = wv.lane();
         wv.sync();
         T m = 0;
-        if (t < N) {
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k < N) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) - ld(L.Y(t) + j)));
+                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(k) + j) - ld(L.Y(k) + j)));
+            }
         }
         return rmax(m);
     }
@@ -1874,9 +2304,12 @@ struct WideSolver {
             const int t = wv.lane();
             wv.sync();
             T m = 0;
-            if (t < N) {
+            for (int b = 0; b < NB; ++b) {
+                const int k = t + 64 * b;
+                if (k < N) {
 #pragma unroll
-                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(t) + j) * rcp(rowscale(j, t))));
+                    for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(k) + j) * rcp(rowscale(j, k))));
+                }
             }
             ymax = rmax(m);
         }
@@ -1884,9 +2317,12 @@ struct WideSolver {
         {
             const int t = wv.lane();
             wv.sync();
-            if (t < N) {
+            for (int b = 0; b < NB; ++b) {
+                const int k = t + 64 * b;
+                if (k < N) {
 #pragma unroll
-                for (int j = 0; j < 6; ++j) st(L.Y(t) + j, use ? ld(L.YP(t) + j) : (T)0);
+                    for (int j = 0; j < 6; ++j) st(L.Y(k) + j, use ? ld(L.YP(k) + j) : (T)0);
+                }
             }
         }
         return do_stats(false, (T)0, (T)0, K_BEGIN);
@@ -2306,12 +2742,13 @@ struct WideSolver {
     }
     MPCG_HD T objective_out() {
         T f = 0;
-        if (t < N) {
-            const int k = t;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
             T s[6];
 #pragma unroll
             for (int j = 0; j < 6; ++j) s[j] = x_state(j, k);
-            f = cost_state(s);
+            f += cost_state(s);
             if (k < N - 1) {
                 const T u[2] = {x_ctrl(0, k), x_ctrl(1, k)};
                 T up[2] = {0, 0};

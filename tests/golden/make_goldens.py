@@ -12,7 +12,7 @@ Fixtures (data only -- inputs and expected outputs):
   infinity_N20.npz   256 infinity-set problems + 32 edge cases, plugin defaults,
                      solved by the oracle (Ipopt restatement, Ipopt default options)
   variants.npz       other parameter sets (class defaults, W_DA = 0, rate penalty on w,
-                     N = 40, N = 3, small BOUND with active state bounds)
+                     N = 40, N = 3, small BOUND with active state bounds, N = 80, N = 100)
   preprocess.npz     findBestPath inputs (poses, waypoints) and the oracle's outputs
   bicycle_N25.npz    the kinematic-bicycle variant (BASELINE configs[4]; no reference
                      implementation exists, so this pins the build's own restatement):
@@ -109,6 +109,9 @@ VARIANTS = {
     "N40": (dict(PLUGIN, STEPS=40), 24, 4000),
     "N3": (dict(PLUGIN, STEPS=3), 16, 5000),
     "small_bound": (dict(PLUGIN, BOUND=0.4), 16, 6000),
+    # the cfg's STEPS range reaches 100 (MPCPlanner.cfg:22): two stage blocks per wavefront
+    "N80": (dict(PLUGIN, STEPS=80), 8, 8000),
+    "N100": (dict(PLUGIN, STEPS=100), 8, 9000),
 }
 
 

@@ -123,6 +123,10 @@ struct HostWave {
     }
     template <class U>
     U uni_d(U v) const { return from(v, 0); }
+    template <class U>
+    U lane63(U v) const { return from(v, 63); }
+    template <class U>
+    U lane0(U v) const { return from(v, 0); }
     // reduction partners of the device (wave_dev.h): xor 1, xor 2, mirror 8, mirror 16, xor 16, xor 32
     template <int s, class U>
     U rpart(U v) const {
@@ -182,7 +186,13 @@ int main() {
                             for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
                     }
                 };
-                if (P.model == 1 && P.N <= 32) {
+                if (P.model == 1 && P.N > 64) {
+                    mpcg::WideSolver<HostWave, 1, false, HT, 2> S(P, pr, wv, spill.data());
+                    run(S);
+                } else if (P.model == 0 && P.N > 64) {
+                    mpcg::WideSolver<HostWave, 0, false, HT, 2> S(P, pr, wv, spill.data());
+                    run(S);
+                } else if (P.model == 1 && P.N <= 32) {
                     mpcg::WideSolver<HostWave, 1, true, HT> S(P, pr, wv, spill.data());
                     run(S);
                 } else if (P.model == 1) {

@@ -102,7 +102,7 @@ def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
     assert (r["status"] == 14).any()
 
 
-@pytest.mark.parametrize("name", ["class_defaults", "rate_w", "N40", "N3", "small_bound"])
+@pytest.mark.parametrize("name", ["class_defaults", "rate_w", "N40", "N3", "small_bound", "N80"])
 def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
     g = variants_golden[name]
     n = 6

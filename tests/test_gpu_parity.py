@@ -90,7 +90,7 @@ def test_infinity_set_matches_oracle(torch_cuda, infinity_golden):
     check_against(r, g)
 
 
-@pytest.mark.parametrize("name", ["class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound"])
+@pytest.mark.parametrize("name", ["class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound", "N80", "N100"])
 def test_variants_match_oracle(torch_cuda, variants_golden, name):
     g = variants_golden[name]
     r = solver_for(params_from_array(g["params"])).solve(g["state"], g["coeffs"])
@@ -220,6 +220,26 @@ def test_bicycle_matches_oracle(torch_cuda, bicycle_golden):
     s = solver_for(g["P"])
     assert s.strategy == "wave"
     check_against(s.solve(g["state"], g["coeffs"]), g)
+
+
+@pytest.mark.parametrize("N", [65, 128])
+def test_two_block_horizons(torch_cuda, oracle, N):
+    """64 < STEPS <= 128: lane t carries stages t and 64 + t (the smallest and the largest
+    two-block horizons), against the oracle."""
+    from mpc_ros_amd import infinity, params
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=N)
+    st, cf = infinity.make_problems(np.arange(9500, 9506))
+    check_against(solver_for(P).solve(st, cf), oracle_ref(oracle, P, st, cf), min_same_iters=0.8)
+
+
+def test_steps_above_128_refused(torch_cuda):
+    from mpc_ros_amd import infinity, params
+    from mpc_ros_amd._lib import MpcgError
+
+    st, cf = infinity.make_problems(np.arange(2))
+    with pytest.raises(MpcgError):
+        solver_for(dict(params.PLUGIN_DEFAULTS, STEPS=129)).solve(st, cf)
 
 
 def test_full_width_N64(torch_cuda, oracle):
