@@ -164,8 +164,9 @@ int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, in
 /* Tracking::findBestPath's preprocessing (mpc_ros/src/driving_state.cpp:175-256) on the
  * device for B robots: waypoints to the vehicle frame, cubic polyfit (Householder QR),
  * cte, heading error from the first int(0.3 M) waypoint increments, delay-mode
- * prediction.  M waypoints per robot, the same for the batch: 4 <= M <= 64 (polyfit asserts
- * order 3 <= M - 1, driving_state.cpp:286).
+ * prediction.  M waypoints per robot, the same for the batch: M >= 4 (polyfit asserts
+ * order 3 <= M - 1, driving_state.cpp:286); plans beyond 64 waypoints take a handle-owned
+ * device scratch of 48 M B bytes (used stream-ordered).
  *   pose [B][3]  x, y, yaw                       (global_pose)
  *   vel  [B][3]  v feedback, previous w, previous throttle (feedback_vel.linear.x, _w, _throttle)
  *   plan [B][M][2] waypoints x, y                (ref_plan)

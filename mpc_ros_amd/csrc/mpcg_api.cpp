@@ -36,6 +36,9 @@ struct mpcg_handle {
     // mpcg_track_device intermediates: state [B][6] | coeffs [B][4] | u0 [B][2]
     double* d_trk = nullptr;
     size_t trk_bytes = 0;
+    // preprocessing scratch of plans longer than 64 waypoints
+    double* d_pp = nullptr;
+    size_t pp_bytes = 0;
     // solve-order buffers (keys, indices, sort scratch)
     void* d_sched = nullptr;
     size_t sched_bytes = 0;
@@ -295,6 +298,7 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->have_last) hipEventSynchronize(h->last_ev);
     if (h->d_io) hipFree(h->d_io);
     if (h->d_trk) hipFree(h->d_trk);
+    if (h->d_pp) hipFree(h->d_pp);
     if (h->d_sched) hipFree(h->d_sched);
     if (h->d_spill) hipFree(h->d_spill);
     if (h->last_ev) hipEventDestroy(h->last_ev);
@@ -487,15 +491,31 @@ int mpcg_preprocess_device(mpcg_handle* h, int64_t B, int32_t M, const double* d
     if (B < 0) return fail(-1, "negative batch");
     if (B == 0) return 0;
     // findBestPath returns without solving for an empty plan (driving_state.cpp:182-185);
-    // polyfit asserts order 3 <= M - 1 (:286)
-    if (M < 4 || M > 64) return fail(-1, "M (waypoints per robot) must be in [4, 64]");
+    // polyfit asserts order 3 <= M - 1 (:286); any longer plan is taken (beyond 64
+    // waypoints through an HBM workspace)
+    if (M < 4) return fail(-1, "M (waypoints per robot) must be >= 4");
     if (!d_pose || !d_vel || !d_plan || !d_state || !d_coeffs) return fail(-1, "null buffer");
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = mpcg::find_best_path_ws_bytes(B, M);
+    if (need > h->pp_bytes) {
+        if (h->d_pp) {
+            hipDeviceSynchronize();  // the old scratch may be in use on any stream
+            hipFree(h->d_pp);
+            h->d_pp = nullptr;
+            h->pp_bytes = 0;
+        }
+        e = hipMalloc((void**)&h->d_pp, need);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(preprocessing scratch)");
+        h->pp_bytes = need;
+    }
+    int rc = need ? order_on(h, s) : 0;
+    if (rc) return rc;
     e = mpcg::launch_find_best_path(B, M, h->params.dt, delay_mode ? 1 : 0, d_pose, d_vel, d_plan, d_state,
-                                    d_coeffs, (hipStream_t)stream);
+                                    d_coeffs, h->d_pp, s);
     if (e != hipSuccess) return hip_fail(e, "find_best_path launch");
-    return 0;
+    return need ? record_on(h, s) : 0;
 }
 
 int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose, const double* d_vel,

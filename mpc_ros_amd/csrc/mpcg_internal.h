@@ -24,8 +24,10 @@ hipError_t launch_wide_order(int64_t B, const double* coeffs, void* buf, size_t 
                              hipStream_t stream);
 
 // findBestPath preprocessing and post-processing (mpcg_track.hip).
+// (M > 64: ws holds find_best_path_ws_bytes(B, M) bytes of device scratch)
+size_t find_best_path_ws_bytes(int64_t B, int M);
 hipError_t launch_find_best_path(int64_t B, int M, double dt, int delay_mode, const double* pose, const double* vel,
-                                 const double* plan, double* state, double* coeffs, hipStream_t stream);
+                                 const double* plan, double* state, double* coeffs, double* ws, hipStream_t stream);
 hipError_t launch_post(int64_t B, double dt, double ref_v, const double* vel, const double* u0, double* cmd,
                        hipStream_t stream);
 

@@ -11,8 +11,9 @@
 //
 // The QR runs on MAXM-row arrays (the M waypoint rows followed by zero rows, which
 // change no norm or inner product), unrolled so they stay in registers for M <= 16;
-// a second instance with MAXM = 64 covers longer plans.  Same operation order as
-// oracle/preprocess.c.
+// a second instance with MAXM = 64 covers longer plans, and plans beyond 64 waypoints
+// (findBestPath takes any length) run the same QR with the matrix in an HBM workspace
+// (k_find_best_path_long).  Same operation order as oracle/preprocess.c.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -84,6 +85,9 @@ struct TrackArgs {
     double* coeffs;       // [B][4]
 };
 
+__device__ __forceinline__ void finish_state(const TrackArgs& a, int64_t p, double theta, double v, double w,
+                                             double throttle, const double* c);
+
 template <int MAXM>
 __global__ void __launch_bounds__(64) k_find_best_path(TrackArgs a) {
     const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -107,6 +111,72 @@ __global__ void __launch_bounds__(64) k_find_best_path(TrackArgs a) {
     }
     double c[4];
     polyfit3<MAXM>(M, xv, yv, c);
+    finish_state(a, p, theta, v, w, throttle, c);
+}
+
+// Plans of more than 64 waypoints: polyfit3's Householder QR, same operations in the same
+// order, on the M x 4 matrix, the right-hand side and the reflector held in HBM
+// (element (i, j) of robot p at ws[(6 i + j) B + p]: a wavefront's lanes touch 64
+// consecutive doubles); zero rows past M change nothing, so the loops stop at M.
+__global__ void __launch_bounds__(64) k_find_best_path_long(TrackArgs a, double* ws) {
+    const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (p >= a.B) return;
+    const int M = a.M;
+    const int64_t B = a.B;
+    double* e = ws + p;
+#define E(i, j) e[((int64_t)(i) * 6 + (j)) * B]
+    const double px = a.pose[p * 3 + 0], py = a.pose[p * 3 + 1], theta = a.pose[p * 3 + 2];
+    const double v = a.vel[p * 3 + 0], w = a.vel[p * 3 + 1], throttle = a.vel[p * 3 + 2];
+    const double* pl = a.plan + p * (int64_t)M * 2;
+    const double ct = cos(theta), st = sin(theta);
+    for (int i = 0; i < M; ++i) {
+        const double dx = pl[2 * i] - px, dy = pl[2 * i + 1] - py;
+        const double xv = dx * ct + dy * st;
+        E(i, 0) = 1.0;
+        double q = 1.0;
+        for (int j = 0; j < 3; ++j) {
+            q = q * xv;
+            E(i, j + 1) = q;
+        }
+        E(i, 4) = dy * ct - dx * st;
+    }
+    for (int k = 0; k < 4; ++k) {
+        double nrm = 0.0;
+        for (int i = k; i < M; ++i) nrm += E(i, k) * E(i, k);
+        nrm = sqrt(nrm);
+        const double akk = E(k, k);
+        const double alpha = (akk > 0) ? -nrm : nrm;
+        double vnorm2 = 0.0;
+        for (int i = k; i < M; ++i) {
+            const double vi = (i == k) ? akk - alpha : E(i, k);
+            E(i, 5) = vi;
+            vnorm2 += vi * vi;
+        }
+        if (nrm == 0.0 || vnorm2 == 0.0) continue;
+        for (int j = k; j < 5; ++j) {  // columns k..3, then the right-hand side
+            double s = 0.0;
+            for (int i = k; i < M; ++i) s += E(i, 5) * E(i, j);
+            s = 2.0 * s / vnorm2;
+            for (int i = k; i < M; ++i) E(i, j) = E(i, j) - s * E(i, 5);
+        }
+    }
+    double c[4];
+    for (int k = 3; k >= 0; --k) {
+        double s = E(k, 4);
+        for (int j = k + 1; j < 4; ++j) s -= E(k, j) * c[j];
+        c[k] = s / E(k, k);
+    }
+#undef E
+    finish_state(a, p, theta, v, w, throttle, c);
+}
+
+// cte, the path heading and the (delayed) state from the fitted polynomial
+// (driving_state.cpp:211-256)
+__device__ __forceinline__ void finish_state(const TrackArgs& a, int64_t p, double theta, double v, double w,
+                                             double throttle, const double* c) {
+    const int M = a.M;
+    const double dt = a.dt;
+    const double* pl = a.plan + p * (int64_t)M * 2;
     // polyeval(coeffs, 0.0) with pow(0, k) (driving_state.cpp:302-309): pow(0, 0) = 1
     const double cte = c[0];
     double gx = 0.0, gy = 0.0;
@@ -162,16 +232,22 @@ __global__ void __launch_bounds__(64) k_post(int64_t B, double dt, double ref_v,
 }
 
 hipError_t launch_find_best_path(int64_t B, int M, double dt, int delay_mode, const double* pose, const double* vel,
-                                 const double* plan, double* state, double* coeffs, hipStream_t stream) {
+                                 const double* plan, double* state, double* coeffs, double* ws, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
     const TrackArgs a{B, M, dt, delay_mode, pose, vel, plan, state, coeffs};
     const dim3 grid((unsigned)((B + 63) / 64)), block(64);
     if (M <= 16)
         hipLaunchKernelGGL(k_find_best_path<16>, grid, block, 0, stream, a);
-    else
+    else if (M <= 64)
         hipLaunchKernelGGL(k_find_best_path<64>, grid, block, 0, stream, a);
+    else if (!ws)
+        return hipErrorInvalidValue;
+    else
+        hipLaunchKernelGGL(k_find_best_path_long, grid, block, 0, stream, a, ws);
     return hipGetLastError();
 }
+
+size_t find_best_path_ws_bytes(int64_t B, int M) { return M > 64 ? sizeof(double) * 6 * (size_t)M * (size_t)B : 0; }
 
 hipError_t launch_post(int64_t B, double dt, double ref_v, const double* vel, const double* u0, double* cmd,
                        hipStream_t stream) {

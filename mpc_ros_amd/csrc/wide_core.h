@@ -1761,6 +1761,7 @@ struct WideSolver {
     // heading error and rows 4, 5: one sine/cosine and half the slacks per lane.  Same
     // per-quantity formulas as the unsplit sweep (trial()).
     MPCG_HD bool trial_split(T alpha, T* phi, T* th) {
+        wv.mark(9);
         const int t = wv.lane();
         const int k = t & 31;
         const bool hi = t >= 32, act = k < N, last = k == N - 1;
@@ -1934,8 +1935,15 @@ struct WideSolver {
         // obj_max_inc: a trial barrier value more than 10^(obj_max_inc basval) above the
         // reference is rejected (log10(phi_t - phi_ref) > obj_max_inc basval, evaluated once
         // per search as the threshold)
-        const T basval = fabs(ref_phi) > (T)10 ? (T)log10((double)fabs(ref_phi)) : (T)1;
-        ref_inc = wv.uni_d((T)pow(10.0, (double)((T)P.obj_max_inc * basval)));
+        // 10^(obj_max_inc log10|phi|) = |phi|^obj_max_inc (|phi| > 10; 10^obj_max_inc else);
+        // the default 5 by products
+        const T b = tmax((T)fabs(ref_phi), (T)10);
+        if (P.obj_max_inc == 5.0) {
+            const T b2 = b * b;
+            ref_inc = wv.uni_d(b2 * b2 * b);
+        } else {
+            ref_inc = wv.uni_d((T)pow((double)b, P.obj_max_inc));
+        }
         if (wv.uni(gd < 0)) {
             ref_pgd = wv.uni_d((T)pow((double)-gd, 2.3));
             ref_pth = wv.uni_d((T)pow((double)th, 1.1));
@@ -2719,6 +2727,7 @@ struct WideSolver {
             } else if (o == OP_TRIAL) {
                 tr_ok = trial(tr_alpha, &tr_phi, &tr_theta);
                 tr_acc = tr_ok && check_acceptability(tr_test, tr_phi, tr_theta);
+                wv.mark(10);
             } else if (o == OP_PDERR) {
                 pd_val = pd_error();
             } else {

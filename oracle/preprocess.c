@@ -9,6 +9,7 @@
  * preprocessing kernel) is checked against this one.
  */
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include "ora.h"
 
@@ -16,9 +17,14 @@
 int ora_polyfit(int M, const double* xs, const double* ys, int order, double* coeffs) {
     const int n = order + 1;
     if (order < 1 || order > 8 || order > M - 1) return -1;
-    double A[64 * 9];
-    double b[64];
-    if (M > 64) return -1;
+    double As[64 * 9], bs[64], vs[64];
+    double *A = As, *b = bs, *vv = vs;
+    if (M > 64) { /* longer plans: the same arrays on the heap */
+        A = (double*)malloc(sizeof(double) * (size_t)M * (size_t)(n + 2));
+        if (!A) return -1;
+        b = A + (size_t)M * n;
+        vv = b + M;
+    }
     for (int i = 0; i < M; ++i) {
         A[i] = 1.0;                                    /* A(i,0) = 1 (:290-291) */
         for (int j = 0; j < order; ++j) A[i + (j + 1) * M] = A[i + j * M] * xs[i]; /* :293-297 */
@@ -31,7 +37,6 @@ int ora_polyfit(int M, const double* xs, const double* ys, int order, double* co
         if (nrm == 0.0) continue;
         double alpha = (A[k + k * M] > 0) ? -nrm : nrm;
         double v0 = A[k + k * M] - alpha;
-        double vv[64];
         vv[k] = v0;
         for (int i = k + 1; i < M; ++i) vv[i] = A[i + k * M];
         double vnorm2 = 0.0;
@@ -53,21 +58,29 @@ int ora_polyfit(int M, const double* xs, const double* ys, int order, double* co
         for (int j = k + 1; j < n; ++j) s -= A[k + j * M] * coeffs[j];
         coeffs[k] = s / A[k + k * M];
     }
+    if (A != As) free(A);
     return 0;
 }
 
 int ora_find_best_path(double px, double py, double theta, double v, double w, double throttle, double dt,
                        int M, const double* plan, int delay_mode, double* state, double* coeffs) {
     if (M <= 0) return -1;                             /* :182-185 */
-    if (M > 64) return -2;
     const double ct = cos(theta), st = sin(theta);
-    double xv[64], yv[64];
+    double xs[64], ys[64];
+    double *xv = xs, *yv = ys;
+    if (M > 64) {
+        xv = (double*)malloc(sizeof(double) * 2 * (size_t)M);
+        if (!xv) return -2;
+        yv = xv + M;
+    }
     for (int i = 0; i < M; ++i) {
         const double dx = plan[2 * i] - px, dy = plan[2 * i + 1] - py;
         xv[i] = dx * ct + dy * st;
         yv[i] = dy * ct - dx * st;
     }
-    if (ora_polyfit(M, xv, yv, 3, coeffs) != 0) return -3;
+    const int rc = ora_polyfit(M, xv, yv, 3, coeffs);
+    if (xv != xs) free(xv);
+    if (rc != 0) return -3;
     double cte = 0.0;
     for (int k = 0; k < 4; ++k) cte += coeffs[k] * pow(0.0, k);   /* polyeval(coeffs, 0.0), :302-309 */
     double etheta = atan(coeffs[1]);

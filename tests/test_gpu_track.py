@@ -79,9 +79,10 @@ def test_preprocess_rejects_short_plans(torch_cuda):
         _run_preprocess(torch_cuda, _solver(), pose, pose, np.zeros((2, 3, 2)))
 
 
-@pytest.mark.parametrize("M", [4, 11, 17, 40, 64])
+@pytest.mark.parametrize("M", [4, 11, 17, 40, 64, 65, 100, 257])
 def test_preprocess_plan_lengths(torch_cuda, oracle, M):
-    """Short, medium and long plans (M > 16 takes the 64-row kernel) against the oracle."""
+    """Short, medium and long plans (M > 16 takes the 64-row kernel, M > 64 the kernel with
+    its QR in an HBM workspace: findBestPath takes any plan length) against the oracle."""
     rng = np.random.default_rng(M)
     B = 96
     pose = np.stack([rng.uniform(-2, 2, B), rng.uniform(-2, 2, B), rng.uniform(-np.pi, np.pi, B)], axis=1)

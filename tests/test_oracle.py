@@ -116,6 +116,26 @@ def test_preprocess_restatement(oracle):
     assert rc == -1  # empty plan (driving_state.cpp:182-185)
 
 
+@pytest.mark.parametrize("M", [64, 65, 300])
+def test_preprocess_long_plans(oracle, M):
+    """findBestPath takes any plan length: the oracle's QR beyond 64 waypoints (heap arrays)
+    against a least-squares fit of the same vehicle-frame points (numpy lstsq)."""
+    rng = np.random.default_rng(M)
+    px, py, yaw = 0.3, -0.2, 0.4
+    s = np.linspace(0.0, 4.0, M)
+    hd = yaw + 0.2 * s
+    plan = np.stack([px + np.cumsum(np.cos(hd)) * s[1], py + np.cumsum(np.sin(hd)) * s[1]], axis=1)
+    plan += rng.normal(0, 1e-3, plan.shape)
+    rc, st, cf = oracle.find_best_path(px, py, yaw, 0.5, 0.1, 0.2, 0.1, plan, False)
+    assert rc == 0
+    dx, dy = plan[:, 0] - px, plan[:, 1] - py
+    xv = dx * np.cos(yaw) + dy * np.sin(yaw)
+    yv = dy * np.cos(yaw) - dx * np.sin(yaw)
+    ref = np.linalg.lstsq(np.vander(xv, 4, increasing=True), yv, rcond=None)[0]
+    np.testing.assert_allclose(cf, ref, rtol=1e-8, atol=1e-9)
+    assert st[4] == cf[0]  # cte = polyeval(c, 0) (no delay)
+
+
 # --------------------------------------------------------- kinematic bicycle (model 1)
 # No reference implementation exists (SURVEY.md §8f): the NLP is pinned by its own
 # derivative consistency (analytic vs central differences of fg) and by the KKT

@@ -1,10 +1,11 @@
 # Build the phase-timing tool (tools/wide_prof.hip, 2 waves per SIMD) against the product
 # sources (name "base") or a modified copy under variants/<name>/ (diagnostic; not product).
-#   bash tools/build_wp.sh base v1 v2 ...   -> tools/wp_<name>
+#   bash tools/build_wp.sh base v1 v2 ...   -> exp/wp_<name>
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$R/exp"
 for v in "$@"; do
-  if [ "$v" = base ]; then inc=$R/mpc_ros_amd/csrc; else inc=$R/variants/$v; fi
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DWPE=2 -I "$inc" "$R/tools/wide_prof.hip" -o "$R/tools/wp_$v" &
+  if [ "$v" = base ]; then inc="-I$R/mpc_ros_amd/csrc -I$R/include"; else inc="-I$R/variants/$v"; fi
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DWPE=2 $inc "$R/tools/wide_prof.hip" -o "$R/exp/wp_$v" &
 done
 wait

@@ -22,7 +22,7 @@ namespace mpcg {
 constexpr int NPH = 14;
 // 9..13: sub-phase stamps of diagnostic variants (variants/stamps)
 const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest",
-                           "st-accept", "st-eval", "st-vars", "ric-M", "ric-KP"};
+                           "pre-trial", "accept-chk", "st-vars", "ric-M", "ric-KP"};
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
@@ -43,7 +43,7 @@ struct ProfWave : DevWaveBase {
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_prof(IpmParams P, int64_t B, const double* state, const double* coeffs,
                                              unsigned long long* acc, int* iters, int* status,
-                                             unsigned long long* times, unsigned int* cnt) {
+                                             unsigned long long* times, unsigned int* cnt, double* spill) {
     const int64_t p = blockIdx.x;
     if (p >= B) return;
     IpmProblem<double> pr;
@@ -56,7 +56,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     wv.last = (unsigned long long)clock64();
     const unsigned long long t0 = wv.last;
     const unsigned long long r0 = wall_clock64();
-    WideSolver<ProfWave, 0, true> S(P, pr, wv);  // (N = 20: SPLIT)
+    const WideLayout Lw(P.N, P.filter_cap, 0);
+    WideSolver<ProfWave, 0, true, double, 1> S(P, pr, wv, spill + p * (int64_t)Lw.spill());  // (N = 20: SPLIT)
     S.solve();
     if (threadIdx.x == 0) {
         times[2 * p] = r0;
@@ -92,7 +93,14 @@ int main(int argc, char** argv) {
     P.N = 20; P.dt = 0.1; P.ref_cte = 0; P.ref_eth = 0; P.ref_v = 1.0;
     P.w_cte = 1000; P.w_eth = 1000; P.w_v = 100; P.w_w = 100; P.w_a = 50; P.w_dw = 0; P.w_da = 10;
     P.max_w = 1.0; P.max_a = 1.0; P.bound = 1000; P.tol = 1e-8; P.bound_relax_factor = 1e-8; P.mu_init = 0.1;
-    P.max_iter = 3000; P.filter_cap = 64;
+    P.max_iter = 3000; P.filter_cap = 64; P.model = 0; P.lf = 0.5;
+    // Ipopt 3.12 defaults and the max_cpu_time budget at N = 20 (mpcg_api.cpp ipopt_defaults, cpu_iter_budget)
+    P.acceptable_tol = 1e-6; P.acceptable_iter = 15; P.acceptable_dual_inf_tol = 1e10;
+    P.acceptable_constr_viol_tol = 1e-2; P.acceptable_compl_inf_tol = 1e-2; P.acceptable_obj_change_tol = 1e20;
+    P.max_soc = 4; P.kappa_soc = 0.99; P.watchdog_trigger = 10; P.watchdog_trial_max = 3;
+    P.soft_resto_factor = 0.9999; P.max_soft_resto_iters = 10; P.obj_max_inc = 5; P.max_filter_resets = 5;
+    P.filter_reset_trigger = 5; P.tiny_step_tol = 10 * 2.220446049250313e-16; P.tiny_step_y_tol = 1e-2;
+    P.dual_inf_tol = 1; P.constr_viol_tol = 1e-4; P.compl_inf_tol = 1e-4; P.cpu_iter_budget = 2215; P.precision = 0;
     double *dst, *dcf;
     unsigned long long* dacc;
     int *dit, *dss;
@@ -104,6 +112,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dss, B * 4));
     unsigned long long* dtm;
     CK(hipMalloc(&dtm, B * 16));
+    double* dspill;
+    CK(hipMalloc(&dspill, (size_t)mpcg::WideLayout(P.N, P.filter_cap, 0).spill() * 8 * B));
     unsigned int* dcnt;
     CK(hipMalloc(&dcnt, B * mpcg::NPH * 4));
     CK(hipMemset(dcnt, 0, B * mpcg::NPH * 4));
@@ -116,7 +126,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss, dtm, dcnt);
+    hipLaunchKernelGGL(mpcg::k_prof, dim3((unsigned)B), dim3(64), lds, 0, P, B, dst, dcf, dacc, dit, dss, dtm, dcnt, dspill);
     CK(hipGetLastError());
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));

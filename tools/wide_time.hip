@@ -42,6 +42,13 @@ int main(int argc, char** argv) {
     P.w_cte = 1000; P.w_eth = 1000; P.w_v = 100; P.w_w = 100; P.w_a = 50; P.w_dw = 0; P.w_da = 10;
     P.max_w = 1.0; P.max_a = 1.0; P.bound = 1000; P.tol = 1e-8; P.bound_relax_factor = 1e-8; P.mu_init = 0.1;
     P.max_iter = 3000; P.filter_cap = 64; P.model = 0; P.lf = 0.5;
+    // Ipopt 3.12 defaults and the max_cpu_time budget at N = 20 (mpcg_api.cpp ipopt_defaults, cpu_iter_budget)
+    P.acceptable_tol = 1e-6; P.acceptable_iter = 15; P.acceptable_dual_inf_tol = 1e10;
+    P.acceptable_constr_viol_tol = 1e-2; P.acceptable_compl_inf_tol = 1e-2; P.acceptable_obj_change_tol = 1e20;
+    P.max_soc = 4; P.kappa_soc = 0.99; P.watchdog_trigger = 10; P.watchdog_trial_max = 3;
+    P.soft_resto_factor = 0.9999; P.max_soft_resto_iters = 10; P.obj_max_inc = 5; P.max_filter_resets = 5;
+    P.filter_reset_trigger = 5; P.tiny_step_tol = 10 * 2.220446049250313e-16; P.tiny_step_y_tol = 1e-2;
+    P.dual_inf_tol = 1; P.constr_viol_tol = 1e-4; P.compl_inf_tol = 1e-4; P.cpu_iter_budget = 2215; P.precision = 0;
     double *dst, *dcf, *du0, *dobj;
     int *dit, *dss;
     CK(hipMalloc(&dst, B * 6 * 8));
@@ -55,6 +62,8 @@ int main(int argc, char** argv) {
     const size_t sb = mpcg::wide_sched_bytes(B);
     void* dsched;
     CK(hipMalloc(&dsched, sb));
+    void* dspill;
+    CK(hipMalloc(&dspill, mpcg::wide_spill_bytes(P, B)));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -64,7 +73,7 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(e0));
         int32_t* order = nullptr;
         CK(mpcg::launch_wide_order(B, dcf, dsched, sb, &order, 0));
-        CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, 0));
+        CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill, 0));
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms = 0;
