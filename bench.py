@@ -23,9 +23,13 @@ traffic = memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the commit
 rocprofv3 PMC summary for this configuration (profiles/pmc_B<B>_N<N>.json), or null.
 The path is not HBM-bound: the kernel is FP64-VALU issue/latency
 bound, so the line also carries valu_fp64 = FP64 FLOP/s (PMC-counted FLOPs per
-solve x solves / kernel time) against the 78.6 TFLOP/s vector peak.
-cpu_baseline: the oracle (dense Ipopt restatement, "port") on a bounded sample of
-the same problems, rank 0, N = 1 only.
+solve x solves / kernel time: physical lane-FLOPs, redundant lanes included) and
+valu_algorithmic = the useful flops of SURVEY.md §8d's formula (iterations x Riccati
+and forward-pass flops per stage) / kernel time, both against the vector peak.
+cpu_baseline: the oracle (the Ipopt restatement, "port") on a bounded sample of the
+same problems, rank 0, N = 1 only: its KKT systems in stage order factored within their
+band (the structured linear algebra, as Ipopt's sparse solver would) as the value, the
+checker's dense factorisation as a second figure.
 """
 from __future__ import annotations
 
@@ -43,6 +47,16 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6
+FP32_VALU_PEAK_TFLOPS = 157.3
+
+
+def algorithmic_flops_per_solve(N: int, iters_mean: float) -> float:
+    """iters x [(N - 1) F_stage + 60 N], F_stage = 4n^3 + 6n^2 m + 4 n m^2 + 2n^2
+    + 4nm of the dense Riccati stage and forward pass at n = 8 (state + previous control),
+    m = 2: 3136 flop."""
+    n, m = 8, 2
+    f_stage = 4 * n ** 3 + 6 * n * n * m + 4 * n * m * m + 2 * n * n + 4 * n * m
+    return iters_mean * ((N - 1) * f_stage + 60 * N)
 
 
 def parse():
@@ -92,27 +106,40 @@ def host_cpu():
     return threads, model
 
 
+def _time_oracle(O, P, st, cf, opts, threads, budget_s):
+    """Solves/s of the oracle on the first problems of the batch within about budget_s."""
+    n = threads * 2
+    t0 = time.perf_counter()
+    O.mpc_solve_batch(P, st[:n], cf[:n], opts=opts, nthreads=threads)
+    per = (time.perf_counter() - t0) / n
+    m = int(max(n, min(len(st), budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    r = O.mpc_solve_batch(P, st[:m], cf[:m], opts=opts, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return m / dt, m, dt, float(np.mean(r["iters"]))
+
+
 def cpu_baseline(P, st, cf, budget_s):
-    """Oracle (Ipopt restatement, dense KKT) timed on the host cores this process may use."""
+    """The Ipopt restatement (oracle/ipm.c) timed on the host cores this process may use:
+    value = its KKT systems in stage order factored within their band (kkt_structured: the
+    cost of Ipopt's sparse LDL^T on this block-tridiagonal system, the same algorithm the
+    GPU runs); dense_value = the checker's dense Bunch-Kaufman, as a second figure."""
     from oracle import pyoracle as O
 
     O.build()
     threads, model = host_cpu()
     opts = O.ref_opts(int(P["STEPS"]))
-    n = threads * 2
-    t0 = time.perf_counter()
-    O.mpc_solve_batch(P, st[:n], cf[:n], opts=opts, nthreads=threads)
-    dt = time.perf_counter() - t0
-    per = dt / n
-    m = int(max(n, min(len(st), budget_s / max(per, 1e-6))))
-    t0 = time.perf_counter()
-    r = O.mpc_solve_batch(P, st[:m], cf[:m], opts=opts, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return dict(value=m / dt, unit="solves/s", cores=threads, kind="port", cpu_model=model,
+    sopts = O.ref_opts(int(P["STEPS"]))
+    sopts.kkt_structured = 1
+    v, m, dt, it = _time_oracle(O, P, st, cf, sopts, threads, budget_s)
+    dv, dm, ddt, _ = _time_oracle(O, P, st, cf, opts, threads, budget_s / 3)
+    return dict(value=v, unit="solves/s", cores=threads, kind="port", cpu_model=model,
                 sample=f"first {m} problems of the benchmark batch, oracle/ipm.c (Ipopt 3.12 algorithm with SOC, "
-                       f"watchdog, restoration; dense Bunch-Kaufman KKT), {threads} OpenMP threads "
-                       f"(sched_getaffinity, capped by OMP_NUM_THREADS), {dt:.1f} s",
-                iters_mean=float(np.mean(r["iters"])))
+                       f"watchdog, restoration) with the KKT matrix in stage order and an envelope Bunch-Kaufman "
+                       f"LDL^T (kkt_structured), {threads} OpenMP threads, one problem per thread "
+                       f"(sched_getaffinity, capped by OMP_NUM_THREADS: the box's CPU share), {dt:.1f} s",
+                iters_mean=it, dense_value=dv,
+                dense_sample=f"first {dm} problems, the checker's dense Bunch-Kaufman KKT, {ddt:.1f} s")
 
 
 def latency_b1(P, st, cf, solver, dev, reps=50):
@@ -329,6 +356,13 @@ def main():
                     "frac": got / FP64_VALU_PEAK_TFLOPS, "flops_per_solve": fl,
                     "source": f"profiles/{prof}.json (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes: physical FP64 "
                               f"lane-FLOPs, replicated and idle lanes included)"}
+        af = algorithmic_flops_per_solve(N, float(it.mean()))
+        got_a = af * count / (kern * 1e-3) / 1e12
+        peak_a = FP64_VALU_PEAK_TFLOPS if a.dtype == "fp64" else FP32_VALU_PEAK_TFLOPS
+        valu_alg = {"achieved": got_a, "peak": peak_a, "unit": "TFLOP/s", "frac": got_a / peak_a,
+                    "flops_per_solve": af,
+                    "source": "SURVEY.md §8d: iters_mean x [(N-1) x 3136 + 60 N] (useful Riccati + forward-pass "
+                              "flops) / kernel time"}
         line = {
             "metric": "NMPC solves/sec (whole node), N=20 diff-drive, at 1/2/4/8 MI355X",
             "value": value,
@@ -353,7 +387,7 @@ def main():
                          "strategy": solver.strategy, "kernel_ms": kern,
                          "algorithmic_bytes_per_solve": bytes_per_solve,
                          "traffic_source": f"profiles/{prof}.json" if traffic else None,
-                         "valu_fp64": valu},
+                         "valu_fp64": valu, "valu_algorithmic": valu_alg},
             "solver": {"iters_mean": float(it.mean()), "iters_max": int(it.max()),
                        "success_frac": float(np.mean(sts == 1))},
         }

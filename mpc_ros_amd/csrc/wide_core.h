@@ -1945,8 +1945,8 @@ struct WideSolver {
             ref_inc = wv.uni_d((T)pow((double)b, P.obj_max_inc));
         }
         if (wv.uni(gd < 0)) {
-            ref_pgd = wv.uni_d((T)pow((double)-gd, 2.3));
-            ref_pth = wv.uni_d((T)pow((double)th, 1.1));
+            ref_pgd = wv.uni_d((T)pow_pos((double)-gd, 2.3));
+            ref_pth = th > 0 ? wv.uni_d((T)pow_pos((double)th, 1.1)) : (T)0;
         }
     }
     MPCG_HD bool is_ftype(T alpha_test) const { return ref_gd < 0 && alpha_test * ref_pgd > ref_pth; }
@@ -2417,6 +2417,7 @@ struct WideSolver {
 
     // K_NEWTON: inertia correction (Algorithm IC); once the system is solved, the line search
     MPCG_HD int k_newton() {
+        wv.mark(11);
         if (!sv_ok) {
             T delta_w = sv_delta;
             if (inertia_attempt == 0)
@@ -2449,6 +2450,7 @@ struct WideSolver {
         else
             set_ref(theta, phik, F.gd);
         lsF = F;
+        wv.mark(12);
         bool tiny = false;
         if (P.tiny_step_tol > 0 && wv.uni(F.rel <= (T)P.tiny_step_tol)) tiny = wv.uni(dy_max() <= (T)P.tiny_step_y_tol);
         if (in_wd && tiny) {
@@ -2734,6 +2736,7 @@ struct WideSolver {
                 soc_rhs(soc_alpha());
             }
             const int s = step(wv.uni(ct));
+            wv.mark(13);
             if (s > 0) {
                 status = s;
                 break;

@@ -266,6 +266,8 @@ struct ipm {
     int resto_first;   /* restoration problem: first convergence check */
     ora_ipm_result* diag;
     double* mem;
+    /* kkt_structured: position of KKT row i in the banded order, envelope of the factor */
+    int *kpos, *klast;
 };
 
 static double amax(int n, const double* v) {
@@ -289,7 +291,7 @@ static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
     S->m = P->m;
     S->K = P->nw + P->m;
     const size_t nw = P->nw, m = P->m, K = S->K;
-    S->mem = (double*)calloc(40 * nw + 20 * m + 2 * m * nw + nw * nw + K * K + 2 * K + 16, sizeof(double));
+    S->mem = (double*)calloc(40 * nw + 20 * m + 2 * m * nw + nw * nw + K * K + 3 * K + 16, sizeof(double));
     double* p = S->mem;
 #define TAKE(ptr, cnt) do { S->ptr = p; p += (cnt); } while (0)
     TAKE(w, nw); TAKE(y, m); TAKE(zL, nw); TAKE(zU, nw);
@@ -298,7 +300,7 @@ static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
     TAKE(wt, nw); TAKE(yt, m); TAKE(zLt, nw); TAKE(zUt, nw);
     TAKE(gf, nw); TAKE(cv, m); TAKE(A, m * nw); TAKE(W, nw * nw); TAKE(gphi, nw); TAKE(rd, nw);
     TAKE(ct, m); TAKE(csoc, m); TAKE(gft, nw); TAKE(At, m * nw); TAKE(rdt, nw);
-    TAKE(KKT, K * K); TAKE(rhs, K);
+    TAKE(KKT, K * K); TAKE(rhs, 2 * K);
     TAKE(wd_w, nw); TAKE(wd_y, m); TAKE(wd_zL, nw); TAKE(wd_zU, nw);
     TAKE(wd_dw, nw); TAKE(wd_dy, m); TAKE(wd_dzL, nw); TAKE(wd_dzU, nw);
     TAKE(acc_w, nw); TAKE(acc_y, m); TAKE(acc_zL, nw); TAKE(acc_zU, nw);
@@ -315,6 +317,8 @@ static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
     S->last_mu = -1.0;
 }
 static void ipm_free(ipm* S) {
+    free(S->kpos);
+    free(S->klast);
     free(S->mem);
     free(S->ipiv);
     free(S->fth);
@@ -533,6 +537,39 @@ static int factor_kkt(ipm* S) {
     int attempt = 0;
     for (;;) {
         memset(S->KKT, 0, sizeof(double) * (size_t)K * K);
+        if (S->kpos) {  /* kkt_structured: the same matrix in the banded order, envelope factor */
+            const int* q = S->kpos;
+#define KL(i, j) S->KKT[(q[i] > q[j] ? q[i] : q[j]) + (size_t)(q[i] > q[j] ? q[j] : q[i]) * K]
+            for (int j = 0; j < nw; ++j)
+                for (int i = j; i < nw; ++i)
+                    if (S->W[(size_t)i * nw + j] != 0.0) KL(i, j) = S->W[(size_t)i * nw + j];
+            for (int i = 0; i < nw; ++i) {
+                double sig = 0.0;
+                if (P->hasL[i]) sig += S->zL[i] / (S->w[i] - P->wl[i]);
+                if (P->hasU[i]) sig += S->zU[i] / (P->wu[i] - S->w[i]);
+                KL(i, i) += sig + delta_w;
+            }
+            for (int r = 0; r < m; ++r) {
+                for (int j = 0; j < nw; ++j)
+                    if (S->A[(size_t)r * nw + j] != 0.0) KL(nw + r, j) = S->A[(size_t)r * nw + j];
+                KL(nw + r, nw + r) = -delta_c;
+            }
+#undef KL
+            int np, nn, nz;
+            ora_ldlt_factor_env(K, S->KKT, S->ipiv, 1e-300, &np, &nn, &nz, S->klast);
+            if (np == nw && nn == m && nz == 0) {
+                if (delta_w > 0) S->dw_last = delta_w;
+                return 1;
+            }
+            if (nz > 0 && delta_c == 0.0) delta_c = 1e-8 * pow(S->mu, 0.25);
+            if (attempt == 0)
+                delta_w = (S->dw_last == 0.0) ? 1e-4 : fmax(1e-20, S->dw_last / 3.0);
+            else
+                delta_w = (S->dw_last == 0.0) ? 100.0 * delta_w : 8.0 * delta_w;
+            ++attempt;
+            if (delta_w > 1e40) return 0;
+            continue;
+        }
         for (int j = 0; j < nw; ++j)
             for (int i = j; i < nw; ++i) S->KKT[i + (size_t)j * K] = S->W[(size_t)i * nw + j];
         for (int i = 0; i < nw; ++i) {
@@ -572,7 +609,14 @@ static void solve_step(ipm* S, const double* crhs, double* dw, double* dy, doubl
         S->rhs[i] = -s;
     }
     for (int r = 0; r < m; ++r) S->rhs[nw + r] = -crhs[r];
-    ora_ldlt_solve(S->K, S->KKT, S->ipiv, S->rhs);
+    if (S->kpos) {
+        double* b = S->rhs + S->K;  /* (a second K-vector after rhs) */
+        for (int i = 0; i < S->K; ++i) b[S->kpos[i]] = S->rhs[i];
+        ora_ldlt_solve_env(S->K, S->KKT, S->ipiv, S->klast, b);
+        for (int i = 0; i < S->K; ++i) S->rhs[i] = b[S->kpos[i]];
+    } else {
+        ora_ldlt_solve(S->K, S->KKT, S->ipiv, S->rhs);
+    }
     for (int i = 0; i < nw; ++i) dw[i] = S->rhs[i];
     for (int r = 0; r < m; ++r) dy[r] = S->rhs[nw + r];
     for (int i = 0; i < nw; ++i) {
@@ -1241,6 +1285,11 @@ int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out
 
     ipm S;
     ipm_alloc(&S, &P, &opts);
+    if (opts.kkt_structured && nlp->kkt_order && mI == 0) {
+        S.kpos = (int*)malloc(sizeof(int) * (size_t)S.K);
+        S.klast = (int*)malloc(sizeof(int) * (size_t)S.K);
+        for (int i = 0; i < S.K; ++i) S.kpos[nlp->kkt_order[i]] = i;
+    }
     int iter = 0;
     S.iter = &iter;
     ora_ipm_result diag;

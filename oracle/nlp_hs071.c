@@ -59,6 +59,7 @@ int ora_hs071_solve(const ora_ipm_opts* opts, double* x4, double* zl4, double* z
     static const double xl[4] = {1.0, 1.0, 1.0, 1.0}, xu[4] = {5.0, 5.0, 5.0, 5.0};
     static const double gl[2] = {25.0, 40.0}, gu[2] = {1.0e19, 40.0};
     ora_nlp nlp;
+    memset(&nlp, 0, sizeof nlp);
     nlp.n = 4;
     nlp.m = 2;
     nlp.ctx = 0;

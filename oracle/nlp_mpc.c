@@ -279,6 +279,22 @@ int ora_mpc_solve_res(const ora_mpc_params* p, const ora_ipm_opts* opts, const d
     nlp.gl = gl;
     nlp.gu = gu;
     nlp.x0 = x0;
+    /* KKT rows in stage order: stage k's state (6), control (2, k < N-1) and its
+     * constraint rows (the initial-state rows at k = 0, the defect into stage k else) --
+     * a band of ~2.5 stages (ora_ipm_opts.kkt_structured) */
+    int* kord = (int*)malloc(sizeof(int) * (size_t)(nx + ng));
+    {
+        int q = 0;
+        for (int k = 0; k < N; ++k) {
+            for (int sv = 0; sv < 6; ++sv) kord[q++] = nx + sv * N + k;  /* c rows into stage k */
+            for (int sv = 0; sv < 6; ++sv) kord[q++] = sv * N + k;       /* state s_k */
+            if (k < N - 1) {
+                kord[q++] = IW(N) + k;
+                kord[q++] = IA(N) + k;
+            }
+        }
+    }
+    nlp.kkt_order = kord;
     double* lam = (double*)malloc(sizeof(double) * (size_t)ng * 2);
     int status = ora_ipm_solve(&nlp, opts, x, zl, zu, lam, lam + ng, res);
     /* outputs, mpc_planner.cpp:388-401 */
@@ -290,6 +306,7 @@ int ora_mpc_solve_res(const ora_mpc_params* p, const ora_ipm_opts* opts, const d
     u0[0] = x[IW(N)];
     u0[1] = x[IA(N)];
     if (xfull) memcpy(xfull, x, sizeof(double) * nx);
+    free(kord);
     free(lam);
     free(buf);
     return status;

@@ -38,6 +38,11 @@ extern "C" {
  * Returns inertia in (npos, nneg, nzero).  tiny: |pivot| <= tiny counts as zero. */
 int ora_ldlt_factor(int n, double* a, int* ipiv, double tiny, int* npos, int* nneg, int* nzero);
 void ora_ldlt_solve(int n, const double* a, const int* ipiv, double* b);
+/* The same factorisation and solve restricted to the matrix envelope (last[n]: the last
+ * possibly nonzero row of each column, computed by the factorisation): bitwise the
+ * dense results for finite data, O(n b^2) for a banded matrix. */
+int ora_ldlt_factor_env(int n, double* a, int* ipiv, double tiny, int* npos, int* nneg, int* nzero, int* last);
+void ora_ldlt_solve_env(int n, const double* a, const int* ipiv, const int* last, double* b);
 
 /* ------------------------------------------------------------ generic NLP --- */
 /* min f(x) s.t. gl <= g(x) <= gu, xl <= x <= xu.  Dense callbacks.
@@ -53,6 +58,10 @@ typedef struct ora_nlp {
     void (*hess)(void* ctx, const double* x, double sigma, const double* lam,
                  double* h);                                          /* dense n x n, full symmetric */
     const double *xl, *xu, *gl, *gu, *x0;
+    /* optional (NULL: none): an order of the n + m KKT rows (variables 0..n-1, then
+     * constraint rows n..n+m-1) in which the KKT matrix is banded -- used by
+     * ora_ipm_opts.kkt_structured */
+    const int* kkt_order;
 } ora_nlp;
 
 typedef struct ora_ipm_opts {
@@ -88,6 +97,12 @@ typedef struct ora_ipm_opts {
     double dual_inf_tol;                /* 1 */
     double constr_viol_tol;             /* 1e-4 */
     double compl_inf_tol;               /* 1e-4 */
+    /* 0 (default, the checker): dense Bunch-Kaufman of the KKT matrix in the NLP's own
+     * order.  1: the KKT matrix in the NLP's kkt_order (stage order for the MPC NLP),
+     * factored within its envelope (ora_ldlt_factor_env) -- the sparse-solver cost of
+     * Ipopt + MUMPS on this band, for the CPU baseline; same algorithm, iterates equal
+     * to rounding (a different pivot order) */
+    int kkt_structured;
 } ora_ipm_opts;
 
 /* Result; status uses CppAD::ipopt::solve_result::status_type numbering

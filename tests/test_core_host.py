@@ -16,6 +16,18 @@ import pytest
 
 from conftest import ROOT, params_from_array
 
+# The emulation runs 64 host threads per problem in lockstep (a std::barrier per lane
+# exchange): ~0.1-0.3 s per solver iteration.  The default CPU run takes representative
+# subsets (every Ipopt mechanism the fixtures exercise stays covered); MPCG_HOST_FULL=1
+# runs every fixture row.  The GPU parity tests run all of them on the device.
+FULL = os.environ.get("MPCG_HOST_FULL", "") == "1"
+
+
+def subset(g, rows):
+    keys = ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")
+    rows = np.arange(len(g["status"])) if FULL else np.asarray(rows)
+    return {k: g[k][rows] for k in keys if k in g}
+
 
 def opts_line(o) -> str:
     """The harness's Ipopt-option line from an oracle IpmOpts (same values both sides)."""
@@ -76,7 +88,7 @@ def wide_harness(tmp_path_factory):
 
 def test_wide_core_matches_oracle_infinity_subset(wide_harness, infinity_golden):
     g = infinity_golden
-    sel = np.r_[0:24, 256:264]  # course samples + edge cases
+    sel = np.r_[0:24, 256:264] if FULL else np.r_[0:8, 256:260]  # course samples + edge cases
     sub = {k: g[k][sel] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
@@ -87,8 +99,11 @@ def test_wide_core_ipopt_features(wide_harness, features_golden, name):
     """Second-order corrections, the watchdog and soft restoration: the device core takes
     the oracle's path iterate for iterate (tests/golden/ipopt_features.npz)."""
     g = features_golden[name]
-    r = run_harness(wide_harness, g["P"], g["state"], g["coeffs"])
-    compare(r, g, atol=1e-9)
+    # (diag columns: second-order corrections, watchdog, soft restoration, restoration)
+    rows = {"N20": [1, 4, 5, 7], "N40": [4, 6, 12], "bicycle": [1, 2, 3]}[name]
+    sub = subset(g, rows)
+    r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
+    compare(r, sub, atol=1e-9)
 
 
 def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
@@ -105,7 +120,7 @@ def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
 @pytest.mark.parametrize("name", ["class_defaults", "rate_w", "N40", "N3", "small_bound", "N80"])
 def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
     g = variants_golden[name]
-    n = 6
+    n = 6 if FULL or name in ("N3", "small_bound", "class_defaults") else 3
     sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
@@ -114,7 +129,7 @@ def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
 def test_wide_core_bicycle_matches_oracle(wide_harness, bicycle_golden):
     """Kinematic-bicycle variant (N = 25) through the wavefront solver."""
     g = bicycle_golden
-    n = 12
+    n = 12 if FULL else 4
     sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
@@ -130,7 +145,7 @@ def test_wide_core_full_width_N64(wide_harness, oracle):
     from mpc_ros_amd import infinity, params
 
     P = dict(params.PLUGIN_DEFAULTS, STEPS=64)
-    sc = infinity.draw_scenarios(np.arange(200, 206))
+    sc = infinity.draw_scenarios(np.arange(200, 206 if FULL else 203))
     px, py, yaw, plan = infinity.scenario_poses(sc)
     st, cf = infinity.find_best_path(px, py, yaw, sc["v"], sc["w_prev"], sc["a_prev"], P["DT"], plan, True)
     g = _oracle_run(oracle, P, st, cf)

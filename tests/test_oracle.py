@@ -216,3 +216,19 @@ def test_oracle_cpu_time_budget(oracle, features_golden):
     np.testing.assert_array_equal(r["status"], g["status"])
     assert set(np.unique(r["status"])) == {1, 14}
     assert r["iters"][r["status"] == 14].min() == int(g["iter_budget"]) + 1
+
+
+def test_structured_kkt_same_iterates(oracle, infinity_golden):
+    """kkt_structured (the CPU baseline's linear algebra: KKT rows in stage order, envelope
+    Bunch-Kaufman) follows the checker's iterates: same statuses and iteration counts,
+    controls to rounding (a different pivot order)."""
+    g = infinity_golden
+    sel = np.r_[0:24, 256:264]
+    P = params_from_array(g["params"])
+    o = oracle.ref_opts(20)
+    o.kkt_structured = 1
+    r = oracle.mpc_solve_batch(P, g["state"][sel], g["coeffs"][sel], opts=o, nthreads=4)
+    np.testing.assert_array_equal(r["status"], g["status"][sel])
+    np.testing.assert_array_equal(r["iters"], g["iters"][sel])
+    ok = g["status"][sel] == 1
+    np.testing.assert_allclose(r["u0"][ok], g["u0"][sel][ok], rtol=0, atol=1e-12)

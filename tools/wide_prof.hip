@@ -22,7 +22,7 @@ namespace mpcg {
 constexpr int NPH = 14;
 // 9..13: sub-phase stamps of diagnostic variants (variants/stamps)
 const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest",
-                           "pre-trial", "accept-chk", "st-vars", "ric-M", "ric-KP"};
+                           "pre-trial", "accept-chk", "newton-in", "setref", "step-out"};
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
