@@ -76,6 +76,56 @@ struct IpmParams {
     int precision;                      // 0: fp64 (Ipopt's); 1: fp32 solver (differential drive)
 };
 
+// The Ipopt 3.12 options the reference leaves at their defaults (mpc_planner.cpp:356-368:
+// only print_level, the derivative mode and max_cpu_time are set), as mpcg_api.cpp's
+// ipopt_defaults fills them.  A kernel instance for exactly these values compiles them as
+// constants (fewer wave-uniform values held through the solve); launch_wide_solve takes
+// it only when every field below equals the handle's option.
+MPCG_HD void ipopt_default_options(IpmParams& q) {
+    q.tol = 1e-8;
+    q.bound_relax_factor = 1e-8;
+    q.mu_init = 0.1;
+    q.max_iter = 3000;
+    q.filter_cap = 64;
+    q.acceptable_tol = 1e-6;
+    q.acceptable_iter = 15;
+    q.acceptable_dual_inf_tol = 1e10;
+    q.acceptable_constr_viol_tol = 1e-2;
+    q.acceptable_compl_inf_tol = 1e-2;
+    q.acceptable_obj_change_tol = 1e20;
+    q.max_soc = 4;
+    q.kappa_soc = 0.99;
+    q.watchdog_trigger = 10;
+    q.watchdog_trial_max = 3;
+    q.soft_resto_factor = 0.9999;
+    q.max_soft_resto_iters = 10;
+    q.obj_max_inc = 5.0;
+    q.max_filter_resets = 5;
+    q.filter_reset_trigger = 5;
+    q.tiny_step_tol = 10.0 * 2.220446049250313e-16;
+    q.tiny_step_y_tol = 1e-2;
+    q.dual_inf_tol = 1.0;
+    q.constr_viol_tol = 1e-4;
+    q.compl_inf_tol = 1e-4;
+}
+inline bool ipopt_options_are_default(const IpmParams& p) {
+    IpmParams q = p;
+    ipopt_default_options(q);
+    return p.tol == q.tol && p.bound_relax_factor == q.bound_relax_factor && p.mu_init == q.mu_init &&
+           p.max_iter == q.max_iter && p.filter_cap == q.filter_cap && p.acceptable_tol == q.acceptable_tol &&
+           p.acceptable_iter == q.acceptable_iter && p.acceptable_dual_inf_tol == q.acceptable_dual_inf_tol &&
+           p.acceptable_constr_viol_tol == q.acceptable_constr_viol_tol &&
+           p.acceptable_compl_inf_tol == q.acceptable_compl_inf_tol &&
+           p.acceptable_obj_change_tol == q.acceptable_obj_change_tol && p.max_soc == q.max_soc &&
+           p.kappa_soc == q.kappa_soc && p.watchdog_trigger == q.watchdog_trigger &&
+           p.watchdog_trial_max == q.watchdog_trial_max && p.soft_resto_factor == q.soft_resto_factor &&
+           p.max_soft_resto_iters == q.max_soft_resto_iters && p.obj_max_inc == q.obj_max_inc &&
+           p.max_filter_resets == q.max_filter_resets && p.filter_reset_trigger == q.filter_reset_trigger &&
+           p.tiny_step_tol == q.tiny_step_tol && p.tiny_step_y_tol == q.tiny_step_y_tol &&
+           p.dual_inf_tol == q.dual_inf_tol && p.constr_viol_tol == q.constr_viol_tol &&
+           p.compl_inf_tol == q.compl_inf_tol;
+}
+
 // Status numbering of CppAD::ipopt::solve_result::status_type
 // (mpc_ros/include/cppad/ipopt/solve_result.hpp:30-46).
 enum : int32_t {

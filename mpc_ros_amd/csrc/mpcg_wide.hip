@@ -33,7 +33,9 @@ struct WideArgs {
 // T: the solver's arithmetic type (double; float for precision 1).  Inputs and outputs
 // stay double at the boundary.
 // NB: stage blocks (2 for 64 < N <= 128, lane t owning stages t and 64 + t).
-template <int MODEL, bool SPLIT, class T, int NB>
+// DEFOPT: the Ipopt options are the reference's defaults (ipopt_default_options), compiled
+// as constants.
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
@@ -45,8 +47,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
     DevWave wv;
     wv.t = t;
-    const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
-    WideSolver<DevWave, MODEL, SPLIT, T, NB> S(a.P, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
+    IpmParams Pk = a.P;
+    if constexpr (DEFOPT) ipopt_default_options(Pk);
+    const WideLayout Lw(Pk.N, Pk.filter_cap, MODEL);
+    WideSolver<DevWave, MODEL, SPLIT, T, NB> S(Pk, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
     S.solve();
     const double o = (double)S.objective_out();
     const int N = a.P.N;
@@ -132,6 +136,8 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     else if (P.model == 1)
         fn = nb == 2 ? (const void*)k_solve_wide<1, false, double, 2>
            : split ? (const void*)k_solve_wide<1, true, double, 1> : (const void*)k_solve_wide<1, false, double, 1>;
+    else if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
+        fn = (const void*)k_solve_wide<0, true, double, 1, true>;
     else
         fn = nb == 2 ? (const void*)k_solve_wide<0, false, double, 2>
            : split ? (const void*)k_solve_wide<0, true, double, 1> : (const void*)k_solve_wide<0, false, double, 1>;

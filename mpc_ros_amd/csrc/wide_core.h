@@ -2060,8 +2060,8 @@ struct WideSolver {
         const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8;
         T a;
         if (ref_gd < 0) {
-            a = tmin(gamma_theta, gamma_phi * ref_theta / -ref_gd);
-            if (ref_theta <= theta_min) a = tmin(a, ref_pth / ref_pgd);
+            a = tmin(gamma_theta, gamma_phi * ref_theta * rcp(-ref_gd));
+            if (ref_theta <= theta_min) a = tmin(a, ref_pth * rcp(ref_pgd));
         } else {
             a = gamma_theta;
         }
@@ -2343,11 +2343,15 @@ struct WideSolver {
         acc_pending = false;
         const int nbnd = 2 * (8 * N - 2);
         const int ng = 6 * N;
-        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) / (T)100;
-        const T scc = tmax((T)100, l1z / (T)nbnd) / (T)100;
-        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
+        // (quotients by v_rcp_f64 + two Newton steps: 1-2 ulp of the division, a fifth of
+        // its instructions; the termination tests are not decided at that resolution)
+        const T sd = tmax((T)100, (l1y + l1z) * rcp((T)(ng + nbnd))) * (T)0.01;
+        const T scc = tmax((T)100, l1z * rcp((T)nbnd)) * (T)0.01;
+        const T isd = rcp(sd), iscc = rcp(scc), isf = rcp(sf);
+        const T dsd = dual_inf * isd;
+        const T E0 = tmax(dsd, tmax(prim_inf, compl0 * iscc));
         // unscaled_curr_dual_infeasibility / _complementarity: objective scaling undone
-        const T dual_uns = dual_inf / sf, compl_uns = compl0 / sf;
+        const T dual_uns = dual_inf * isf, compl_uns = compl0 * isf;
         kkt() = wv.uni_d(tmax(dual_uns, tmax(prim_uns, compl_uns)));
         // CurrentIsAcceptable (objective bookkeeping once per iteration)
         last_obj() = curr_obj();
@@ -2355,8 +2359,8 @@ struct WideSolver {
         cur_acceptable = wv.uni(E0 <= (T)P.acceptable_tol && dual_uns <= (T)P.acceptable_dual_inf_tol &&
                                 prim_uns <= (T)P.acceptable_constr_viol_tol &&
                                 compl_uns <= (T)P.acceptable_compl_inf_tol &&
-                                fabs(last_obj() - curr_obj()) / tmax((T)1, (T)fabs(curr_obj())) <=
-                                    (T)P.acceptable_obj_change_tol);
+                                fabs(last_obj() - curr_obj()) <=
+                                    (T)P.acceptable_obj_change_tol * tmax((T)1, (T)fabs(curr_obj())));
 #ifdef MPCG_TRACE
         if (wv.lane() == 0)
             printf("it %d mu %.3e E0 %.3e dual %.3e prim %.3e compl %.3e duns %.3e puns %.3e cuns %.3e th %.3e\n", iter,
@@ -2388,7 +2392,7 @@ struct WideSolver {
         tiny_flag = 0;
         bool done = false;
         T complmu = tmax(pmax - mu, mu - pmin);
-        T Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+        T Emu = tmax(dsd, tmax(prim_inf, complmu * iscc));
         while (wv.uni((Emu <= kappa_eps * mu || tf) && !done)) {
             const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
             const bool changed = mnew != mu;
@@ -2399,7 +2403,7 @@ struct WideSolver {
                 done = true;
             } else {
                 complmu = tmax(pmax - mu, mu - pmin);
-                Emu = tmax(dual_inf / sd, tmax(prim_inf, complmu / scc));
+                Emu = tmax(dsd, tmax(prim_inf, complmu * iscc));
                 done = Emu > kappa_eps * mu;
             }
             if (done && changed) {  // BacktrackingLineSearch::Reset

@@ -282,3 +282,22 @@ def test_solve_multi_one_gpu_matches_single(torch_cuda, infinity_golden):
     s = solver_for(P).solve(g["state"], g["coeffs"])
     for k in ("u0", "traj", "status", "iters", "obj"):
         np.testing.assert_array_equal(r[k], s[k])
+
+
+def test_default_option_instance_equals_general(torch_cuda, features_golden, oracle):
+    """The kernel instance that compiles the reference's (default) Ipopt options as
+    constants and the general instance (taken for any other option values) run the same
+    solver: an option change that cannot act (acceptable_obj_change_tol 1e20 -> 1e30)
+    takes the general instance and must give bitwise the same results; an option that acts
+    (no second-order corrections, no watchdog) must match the oracle under that option."""
+    g = features_golden["N20"]
+    a = solver_for(g["P"]).solve(g["state"], g["coeffs"])
+    b = solver_for(g["P"], acceptable_obj_change_tol=1e30).solve(g["state"], g["coeffs"])
+    for k in ("u0", "traj", "status", "iters", "obj"):
+        np.testing.assert_array_equal(a[k], b[k])
+    c = solver_for(g["P"], max_soc=0, watchdog_shortened_iter_trigger=0).solve(g["state"], g["coeffs"])
+    o = oracle.ref_opts(20)
+    o.max_soc = 0
+    o.watchdog_shortened_iter_trigger = 0
+    ref = oracle.mpc_solve_batch(g["P"], g["state"], g["coeffs"], opts=o, nthreads=8, diag=True)
+    check_against(c, ref, min_same_iters=1.0)
