@@ -160,3 +160,68 @@ def test_track_tick_equals_solve_on_preprocessed_inputs(torch_cuda):
     s.solve_device(st, cf, u0)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(cmd[:, 1:].cpu().numpy(), u0.cpu().numpy())
+
+
+def test_track_tick_long_plans_match_oracle(torch_cuda, oracle):
+    """A whole control tick with plans of 120 waypoints (the preprocessing's HBM-workspace
+    QR): commands against the oracle pipeline."""
+    torch = torch_cuda
+    from mpc_ros_amd import params
+
+    P = params.PLUGIN_DEFAULTS
+    rng = np.random.default_rng(120)
+    B, M = 48, 120
+    pose = np.stack([rng.uniform(-1, 1, B), rng.uniform(-1, 1, B), rng.uniform(-np.pi, np.pi, B)], axis=1)
+    vel = np.stack([rng.uniform(0.2, 0.8, B), rng.uniform(-0.5, 0.5, B), rng.uniform(-0.5, 0.5, B)], axis=1)
+    s = np.linspace(0.0, 3.0, M)
+    plan = np.empty((B, M, 2))
+    for b in range(B):
+        hd = pose[b, 2] + rng.uniform(-0.2, 0.2) + rng.uniform(-0.3, 0.3) * s
+        plan[b, :, 0] = pose[b, 0] + np.cumsum(np.cos(hd)) * (s[1] - s[0])
+        plan[b, :, 1] = pose[b, 1] + np.cumsum(np.sin(hd)) * (s[1] - s[0])
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+    cmd = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    _solver(P).track_device(t(pose), t(vel), t(plan), cmd, status=status)
+    torch.cuda.synchronize()
+    cmd = cmd.cpu().numpy()
+    sts, cfs = [], []
+    for b in range(B):
+        rc, ost, ocf = oracle.find_best_path(*pose[b], *vel[b], P["DT"], plan[b], True)
+        assert rc == 0
+        sts.append(ost)
+        cfs.append(ocf)
+    ref = oracle.mpc_solve_batch(P, np.array(sts), np.array(cfs), opts=oracle.ref_opts(int(P["STEPS"])), nthreads=16)
+    ok = ref["status"] == 1
+    np.testing.assert_allclose(cmd[ok, 1], ref["u0"][ok, 0], atol=1e-7)
+    np.testing.assert_allclose(cmd[ok, 2], ref["u0"][ok, 1], atol=1e-7)
+
+
+def test_two_streams_share_one_handle(torch_cuda):
+    """One handle, two streams, batches above the solve-order threshold (its sort scratch,
+    spill areas and track buffers are the handle's): the second solve is queued without a
+    host sync and waits on the first one's scratch use; both equal their solo results."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity
+
+    B = 8192
+    dev = torch.device("cuda:0")
+    s = _solver()
+    ins = []
+    for off in (0, 100000):
+        st, cf = infinity.make_problems(np.arange(off, off + B))
+        ins.append((torch.from_numpy(st).to(dev), torch.from_numpy(cf).to(dev)))
+    solo = []
+    for st, cf in ins:
+        u = torch.empty((B, 2), dtype=torch.float64, device=dev)
+        s.solve_device(st, cf, u)
+        torch.cuda.synchronize()
+        solo.append(u.cpu().numpy())
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = [torch.empty((B, 2), dtype=torch.float64, device=dev) for _ in ins]
+    s.solve_device(ins[0][0], ins[0][1], outs[0], stream=s1)
+    s.solve_device(ins[1][0], ins[1][1], outs[1], stream=s2)
+    torch.cuda.synchronize()
+    for o, r in zip(outs, solo):
+        np.testing.assert_array_equal(o.cpu().numpy(), r)
