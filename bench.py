@@ -108,7 +108,7 @@ def host_cpu():
 
 def _time_oracle(O, P, st, cf, opts, threads, budget_s):
     """Solves/s of the oracle on the first problems of the batch within about budget_s."""
-    n = threads * 2
+    n = threads * 8  # (pilot: long enough that thread start-up does not inflate the estimate)
     t0 = time.perf_counter()
     O.mpc_solve_batch(P, st[:n], cf[:n], opts=opts, nthreads=threads)
     per = (time.perf_counter() - t0) / n
