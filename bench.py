@@ -300,6 +300,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     k_ms = []
 
+    g_ms = []
+
     def step(timed):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -316,6 +318,10 @@ def main():
             g_st = D.gather_rows(status, total)
             if a.gather_traj:
                 D.gather_rows(traj.view(count, -1), total)
+            if timed:  # (the collectives are stream-ordered before this event)
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record(stream)
+                g_ms.append((e1, e2))
             return g_u0, g_st
         return u0, status
 
@@ -332,10 +338,16 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern = float(np.mean([e0.elapsed_time(e1) for e0, e1 in k_ms])) if k_ms else float("nan")
+    gath = float(np.mean([e1.elapsed_time(e2) for e1, e2 in g_ms])) if g_ms else 0.0
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed, kern], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern = float(t[0]), float(t[1])
+        # per-rank kernel and gather times, then the max over ranks
+        mine = torch.tensor([elapsed, kern, gath], dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        allr = torch.stack(allr).cpu().numpy()
+        per_rank = {"kernel_ms": allr[:, 1].tolist(), "gather_ms": allr[:, 2].tolist()}
+        elapsed, kern, gath = float(allr[:, 0].max()), float(allr[:, 1].max()), float(allr[:, 2].max())
     if a.mode == "track":  # iteration counts of the same problems
         solver.solve_device(tst, tcf, u0, None, None, None, iters, stream=stream)
         torch.cuda.synchronize()
@@ -390,6 +402,7 @@ def main():
                          "valu_fp64": valu, "valu_algorithmic": valu_alg},
             "solver": {"iters_mean": float(it.mean()), "iters_max": int(it.max()),
                        "success_frac": float(np.mean(sts == 1))},
+            "timing": {"kernel_ms": kern, "gather_ms": gath, "per_rank": per_rank},
         }
         if world == 1 and a.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(P, st, cf, a.cpu_seconds)

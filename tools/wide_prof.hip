@@ -19,10 +19,10 @@
 #include "wide_core.h"
 
 namespace mpcg {
-constexpr int NPH = 14;
+constexpr int NPH = 18;
 // 9..13: sub-phase stamps of diagnostic variants (variants/stamps)
 const char* kPhase[NPH] = {"stats", "ric-pre", "ric-sweep", "fwd-seq", "fwd-adj", "fwd-par", "trial", "ls-rest", "begin-rest",
-                           "pre-trial", "accept-chk", "newton-in", "setref", "step-out"};
+                           "pre-trial", "accept-chk", "newton-in", "setref", "step-out", "pre-filter", "filter-add", "pre-lsfin", "pre-kbt"};
 
 struct ProfWave : DevWaveBase {
     unsigned long long* acc;
