@@ -1,4 +1,4 @@
-# Phase timing (tools/wp_<variant>) at B = 256 (one wavefront per SIMD) and 65536.
+# Phase timing (exp/wp_<variant>, tools/build_wp.sh) at B = 256 (one wavefront per SIMD) and 65536.
 #   WP_VARIANTS="base v1" bash tools/gpu_wp.sh
 set -u
 R=$GRAFT_REPO_ROOT

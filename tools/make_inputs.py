@@ -1,4 +1,4 @@
-"""Write the benchmark batch as tools/inputs_<B>.bin ([int64 B][B x 6 state][B x 4 coeffs]),
+"""Write the benchmark batch as <outdir>/inputs_<B>.bin (default tools/, the tools use exp/) ([int64 B][B x 6 state][B x 4 coeffs]),
 the input format of the diagnostic tools (wide_time.hip, wide_prof.hip).
 
     python tools/make_inputs.py [B] [outdir]
