@@ -233,6 +233,18 @@ def test_two_block_horizons(torch_cuda, oracle, N):
     check_against(solver_for(P).solve(st, cf), oracle_ref(oracle, P, st, cf), min_same_iters=0.8)
 
 
+@pytest.mark.parametrize("N", [2, 32, 33])
+def test_split_boundary_horizons(torch_cuda, oracle, N):
+    """The smallest horizon the reference allows (STEPS = 2: one control stage) and both
+    sides of the half-wave split's limit (32: split sweeps, 33: unsplit), against the
+    oracle."""
+    from mpc_ros_amd import infinity, params
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=N)
+    st, cf = infinity.make_problems(np.arange(9600, 9612))
+    check_against(solver_for(P).solve(st, cf), oracle_ref(oracle, P, st, cf), min_same_iters=0.9)
+
+
 def test_steps_above_128_refused(torch_cuda):
     from mpc_ros_amd import infinity, params
     from mpc_ros_amd._lib import MpcgError
