@@ -41,34 +41,34 @@ namespace mpcg {
 //
 // Stage-major arrays are read and written by stage-parallel lanes (lane k = stage k)
 // with 16-byte accesses.  Their strides are 2 mod 4 doubles (10 for the 8-entry
-// records, 6 for the 6-entry multipliers, 18 for the 16 gains, 42 / 46 for the stage
+// records, 6 for the 6-entry multipliers, 18 for the gain record, 38 / 42 for the stage
 // table) so that the 16 lanes of a ds_read_b128 group and the 8 lanes of a
 // ds_write_b128 group hit distinct LDS banks; at a 64-byte stride they conflict 4-way.
 struct WideLayout {
-    int N, cap, SS;  // SS: stage table stride (42; 46 with the bicycle's turn terms)
-    MPCG_HD WideLayout(int N_, int cap_, int model) : N(N_), cap(cap_), SS(model == 1 ? 46 : 42) {}
+    int N, cap, SS;  // SS: stage table stride (38; 42 with the bicycle's turn terms)
+    MPCG_HD WideLayout(int N_, int cap_, int model) : N(N_), cap(cap_), SS(model == 1 ? 42 : 38) {}
     static constexpr int WS = 10, YS = 6, KS = 18;
     // stage table entries
     static constexpr int SA = 0;    // a[7]: non-trivial entries of A_k (Lin::jac)
     static constexpr int SDT = 7;   // dt
     static constexpr int SD = 8;    // d[6]: F(s_k, u_k) - s_{k+1} (Newton mode)
-    static constexpr int SKF = 14;  // kff[2]
-    static constexpr int SQD = 16;  // diag of the stage Hessian (6 states, 2 controls = R)
-    static constexpr int SQV = 24;  // gradient q (6) and r (2)
-    static constexpr int SCV = 32;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
-    static constexpr int SCC = 37;  // (unused: the rate coupling is a per-lane constant of the sweep)
-    static constexpr int SZERO = 39, SONE = 40, SMONE = 41;  // constants 0, 1, -1
+    static constexpr int SQD = 14;  // diag of the stage Hessian (6 states, 2 controls = R)
+    static constexpr int SQV = 22;  // gradient q (6) and r (2)
+    static constexpr int SCV = 30;  // curvature of the constraints: Q00 Q22 Q32 Q55 Q53
+    static constexpr int SZERO = 35, SONE = 36, SMONE = 37;  // constants 0, 1, -1
+    // (the feed-forward gains kff[2] are the last two doubles of the gain record: KR(k) + KF)
+    static constexpr int KF = 16;
     // bicycle only: model terms of the heading rows (th, eth): d(turn)/d(w) (B_hat
     // column w: v/lf dt; dt for the differential drive), d(turn)/d(v) (A_hat column v:
     // w/lf dt; 0), and the (v, w) curvature of the Lagrangian (-(y_th + y_eth)/lf dt; 0)
-    static constexpr int STW = 42, STV = 43, SHVD = 44;
+    static constexpr int STW = 38, STV = 39, SHVD = 40;
     MPCG_HD int W(int k) const { return WS * k; }
     MPCG_HD int ZL(int k) const { return WS * (N + k); }
     MPCG_HD int ZU(int k) const { return WS * (2 * N + k); }
     MPCG_HD int DW(int k) const { return WS * (3 * N + k); }
     MPCG_HD int Y(int k) const { return 4 * WS * N + YS * k; }
     MPCG_HD int YP(int k) const { return (4 * WS + YS) * N + YS * k; }
-    MPCG_HD int KR(int k) const { return (4 * WS + 2 * YS) * N + KS * k; }  // K[0][0..7] K[1][0..7]
+    MPCG_HD int KR(int k) const { return (4 * WS + 2 * YS) * N + KS * k; }  // K[0][0..7] K[1][0..7] kff[2]
     MPCG_HD int ST(int k) const { return (4 * WS + 2 * YS + KS) * N + SS * k; }
     // scratch of the Riccati sweep: G^T of the stage, then M^T (M[r][c] at MS c + r) in
     // the same 8 columns, MS = 10 doubles apart (16-byte column reads of different
@@ -1188,8 +1188,8 @@ struct WideSolver {
         // the gains' store at ga0 + gak * k: lanes 0..15 K[0][j], K[1][j], lanes 16, 17 k;
         // the other lanes store into their own slot of the G staging, which they
         // overwrite right after
-        const int ga0 = t < 16 ? L.KR(0) + t : (t < 18 ? L.ST(0) + W_::SKF + (t - 16) : sm + MS * i + j);
-        const int gak = t < 16 ? WideLayout::KS : (t < 18 ? L.SS : 0);
+        const int ga0 = t < 18 ? L.KR(0) + t : sm + MS * i + j;
+        const int gak = t < 18 ? WideLayout::KS : 0;
         // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
         const int hvj = j == 3 ? W_::SHVD : W_::SZERO, hvi = i == 3 ? W_::SHVD : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
@@ -1391,7 +1391,7 @@ struct WideSolver {
         T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
         if (ks < N - 1) {
             ldv<16>(L.KR(ks), K);
-            ldv<2>(L.ST(ks) + WideLayout::SKF, kf);
+            ldv<2>(L.KR(ks) + WideLayout::KF, kf);
             ldv<8>(L.ST(ks) + WideLayout::SA, a);
             ldv<6>(L.ST(ks) + WideLayout::SD, d);
             if constexpr (MODEL == 1)
@@ -1581,7 +1581,7 @@ struct WideSolver {
             T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
             if (ks < N - 1) {
                 ldv<16>(L.KR(ks), K);
-                ldv<2>(L.ST(ks) + WideLayout::SKF, kf);
+                ldv<2>(L.KR(ks) + WideLayout::KF, kf);
                 ldv<8>(L.ST(ks) + WideLayout::SA, a);
                 ldv<6>(L.ST(ks) + WideLayout::SD, d);
                 if constexpr (MODEL == 1)
