@@ -56,7 +56,11 @@ def stale() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not stale():
         return LIB
+    # (-disable-promote-alloca-to-lds: the solver owns the whole dynamic LDS from address 0;
+    # the backend would otherwise move a private array into static LDS, which the launch
+    # refuses -- mpcg_wide.hip checks sharedSizeBytes == 0)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-disable-promote-alloca-to-lds",
            "-Wno-unused-result", "-Wno-unused-value",
            f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"']
     if verbose:

@@ -81,7 +81,10 @@ struct WideLayout {
     MPCG_HD int FI() const { return RSC() + 24; }
     MPCG_HD int C0() const { return FI() + 2 * cap; }  // -c of the initial-state rows (6) + pad
     MPCG_HD int CTL() const { return C0() + 8; }       // 16 wave-uniform solver scalars (WideSolver::CtlRef)
-    MPCG_HD int total() const { return CTL() + 16; }
+    // the problem data: initial state (6), polynomial coefficients (4, 16-byte aligned), pad
+    MPCG_HD int PRB() const { return CTL() + 16; }
+    MPCG_HD int PRC() const { return PRB() + 6; }
+    MPCG_HD int total() const { return PRB() + 12; }
     // Per-problem HBM spill area (doubles) of the rare paths: the watchdog's stored iterate
     // and direction (LDS [W(0), YP(N)) = 52N), the last acceptable iterate (W: 10N), the
     // Newton direction kept while second-order corrections are tried (DW, YP: 16N), the
@@ -206,6 +209,18 @@ struct WideSolver {
 
     // ------------------------------------------------------------ LDS helpers
     MPCG_HD T ld(int i) const { return wv.template Sp<T>()[i]; }
+    // the problem data, stored in LDS by setup(): held in registers across the solve it
+    // was spilled around the sweeps that read it
+    struct C4 {
+        T c[4];
+    };
+    MPCG_HD C4 pcoef() const {
+        C4 r;
+        wv.ld2(L.PRC(), r.c[0], r.c[1]);
+        wv.ld2(L.PRC() + 2, r.c[2], r.c[3]);
+        return r;
+    }
+    MPCG_HD T pinit(int j) const { return ld(L.PRB() + j); }
     MPCG_HD void st(int i, T v) const { wv.template Sp<T>()[i] = v; }
     template <int n>
     MPCG_HD void ldn(int i, T* v) const {
@@ -358,6 +373,10 @@ struct WideSolver {
                 st(L.RSC() + 6 + j, rb[j]);
             }
             st(L.RSC() + 12, 1);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) st(L.PRB() + j, pr.init[j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) st(L.PRC() + j, pr.c[j]);
         }
         if (t < 8) st(L.ZB() + t, 0);
     }
@@ -483,9 +502,10 @@ struct WideSolver {
                     sc_t(hi ? w[5] : w[2], &sa, &ca);
                 }
                 const T x = w[0], v = w[3];
-                const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
-                f1 = pr.c[1] + (T)2 * pr.c[2] * x + (T)3 * pr.c[3] * x * x;
-                const T f2 = (T)2 * pr.c[2] + (T)6 * pr.c[3] * x;
+                const C4 pcoef_ = pcoef();
+                const T fx = pcoef_.c[0] + pcoef_.c[1] * x + pcoef_.c[2] * (x * x) + pcoef_.c[3] * (x * x * x);
+                f1 = pcoef_.c[1] + (T)2 * pcoef_.c[2] * x + (T)3 * pcoef_.c[3] * x * x;
+                const T f2 = (T)2 * pcoef_.c[2] + (T)6 * pcoef_.c[3] * x;
                 // Lin::jac: lower a0..a3 (x, y rows), upper a4..a6 (cte row)
                 A[0] = hi ? f1 : -w[3] * sa * dt;
                 A[1] = hi ? sa * dt : ca * dt;
@@ -545,7 +565,7 @@ struct WideSolver {
                 if (q < nr) {
                     const int j = j0 + q;
                     const T wj = hi ? w[4 + q] : w[q];
-                    const T c = k == 0 ? wj - (hi ? pr.init[4 + q] : pr.init[q]) : wj - Fprev[q];
+                    const T c = k == 0 ? wj - pinit(hi ? 4 + q : q) : wj - Fprev[q];
                     if (k == 0) st(L.C0() + j, -c);  // initial-state rows of the Newton system
                     const T rsc = rowscale(j, k);
                     const T cs = rsc * c;
@@ -655,7 +675,7 @@ struct WideSolver {
                 up[0] = ld(L.W(k + 1) + 6);
                 up[1] = ld(L.W(k + 1) + 7);
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 ln.jac(w, dt, a);
                 next_m(ln, w, w + 6, Fk);
                 turn_d(w, w + 6, &twk, &tvk);
@@ -697,7 +717,7 @@ struct WideSolver {
         if (act) {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                const T c = k == 0 ? w[j] - pinit(j) : w[j] - Fprev[j];
                 if (k == 0) st(L.C0() + j, -c);  // initial-state rows of the Newton system
                 const T rsc = rowscale(j, k);
                 const T cs = rsc * c;
@@ -775,7 +795,7 @@ struct WideSolver {
                 if (!last) {
                     ldn<6>(L.Y(k + 1), yn);
                     Lin<T> ln;
-                    ln.eval(pr.c, w);
+                    ln.eval(pcoef().c, w);
                     ln.jac(w, dt, a);
                     next_m(ln, w, w + 6, Fk[b]);
                     turn_d(w, w + 6, &twk, &tvk);
@@ -834,7 +854,7 @@ struct WideSolver {
             }
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[b][j];
+                const T c = k == 0 ? w[j] - pinit(j) : w[j] - Fprev[b][j];
                 if (k == 0) st(L.C0() + j, -c);
                 const T rsc = rowscale(j, k);
                 const T cs = rsc * c;
@@ -940,7 +960,7 @@ struct WideSolver {
                 up[1] = ld(L.W(k + 1) + 7) + alpha * ld(L.DW(k + 1) + 7);
                 f += cost_ctrl(k, w + 6, up);
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 next_m(ln, w, w + 6, Fk[b]);
             }
         }
@@ -952,7 +972,7 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const T wj = ld(L.W(k) + j) + alpha * ld(L.DW(k) + j);
-                const T c = k == 0 ? wj - pr.init[j] : wj - Fprev[b][j];
+                const T c = k == 0 ? wj - pinit(j) : wj - Fprev[b][j];
                 thv += fabs(rowscale(j, k) * c);
             }
         }
@@ -985,7 +1005,7 @@ struct WideSolver {
             T a[7] = {0, 0, 0, 0, 0, 0, 0}, tw = dt, tv = 0;
             if (!last) {
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 ln.jac(w, dt, a);
                 turn_d(w, w + 6, &tw, &tv);
             }
@@ -1077,7 +1097,7 @@ struct WideSolver {
             T a[7] = {0, 0, 0, 0, 0, 0, 0}, tw = dt, tv = 0;
             if (!last) {
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 ln.jac(w, dt, a);
                 turn_d(w, w + 6, &tw, &tv);
             }
@@ -1806,7 +1826,8 @@ struct WideSolver {
                 c_sa = sa;
                 c_ca = ca;
                 const T x = w[0];
-                const T fx = pr.c[0] + pr.c[1] * x + pr.c[2] * (x * x) + pr.c[3] * (x * x * x);
+                const C4 pcoef_ = pcoef();
+                const T fx = pcoef_.c[0] + pcoef_.c[1] * x + pcoef_.c[2] * (x * x) + pcoef_.c[3] * (x * x * x);
                 T turn = w[6] * dt;
                 if (model == 1) turn = w[3] * w[6] / lf * dt;
                 Fa[0] = (hi ? fx - w[1] : w[0]) + w[3] * (hi ? sa : ca) * dt;
@@ -1826,7 +1847,7 @@ struct WideSolver {
                 if (q < nr) {
                     const int j = hi ? 4 + q : q;
                     const T wj = hi ? w[4 + q] : w[q];
-                    const T c = k == 0 ? wj - (hi ? pr.init[4 + q] : pr.init[q]) : wj - Fprev[q];
+                    const T c = k == 0 ? wj - pinit(hi ? 4 + q : q) : wj - Fprev[q];
                     thv += fabs(rowscale(j, k) * c);
                 }
             }
@@ -1878,7 +1899,7 @@ struct WideSolver {
                 up[1] = ld(L.W(k + 1) + 7) + alpha * ld(L.DW(k + 1) + 7);
                 f += cost_ctrl(k, w + 6, up);
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 next_m(ln, w, w + 6, Fk);
             }
         }
@@ -1888,7 +1909,7 @@ struct WideSolver {
         if (act) {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                const T c = k == 0 ? w[j] - pr.init[j] : w[j] - Fprev[j];
+                const T c = k == 0 ? w[j] - pinit(j) : w[j] - Fprev[j];
                 thv += fabs(rowscale(j, k) * c);
             }
         }
@@ -2091,14 +2112,14 @@ struct WideSolver {
 #pragma unroll
                 for (int j = 0; j < 6; ++j) wn[j] = cwn[j] + alpha * cdn[j];
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 T F[6];
                 next_m(ln, w, w + 6, F);
 #pragma unroll
                 for (int j = 0; j < 6; ++j) dn[j] = F[j] - wn[j];
             }
 #pragma unroll
-            for (int j = 0; j < 6; ++j) c0[j] = -(w[j] - pr.init[j]);
+            for (int j = 0; j < 6; ++j) c0[j] = -(w[j] - pinit(j));
         }
         if (k < N - 1) {
             const int sb = L.ST(k) + WideLayout::SD;
@@ -2139,7 +2160,7 @@ struct WideSolver {
                 up[0] = ld(L.W(k + 1) + 6);
                 up[1] = ld(L.W(k + 1) + 7);
                 Lin<T> ln;
-                ln.eval(pr.c, w);
+                ln.eval(pcoef().c, w);
                 ln.jac(w, dt, a);
                 next_m(ln, w, w + 6, Fk[b]);
                 turn_d(w, w + 6, &twk, &tvk);
@@ -2174,7 +2195,7 @@ struct WideSolver {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const T wj = ld(L.W(k) + j);
-                const T c = k == 0 ? wj - pr.init[j] : wj - Fprev[b][j];
+                const T c = k == 0 ? wj - pinit(j) : wj - Fprev[b][j];
                 pr_ += fabs(rowscale(j, k) * c);
             }
         }

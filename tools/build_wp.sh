@@ -6,6 +6,6 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$R/exp"
 for v in "$@"; do
   if [ "$v" = base ]; then inc="-I$R/mpc_ros_amd/csrc -I$R/include"; else inc="-I$R/variants/$v"; fi
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DWPE=2 $inc "$R/tools/wide_prof.hip" -o "$R/exp/wp_$v" &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -disable-promote-alloca-to-lds -DWPE=2 $inc "$R/tools/wide_prof.hip" -o "$R/exp/wp_$v" &
 done
 wait
