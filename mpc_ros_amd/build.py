@@ -63,16 +63,37 @@ def build(force: bool = False, verbose: bool = False) -> str:
            "-mllvm", "-disable-promote-alloca-to-lds",
            "-Wno-unused-result", "-Wno-unused-value",
            f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"']
-    if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
+    cmd.append("-Rpass-analysis=kernel-resource-usage")
     cmd += SOURCES + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     if verbose:
         sys.stderr.write(r.stderr)
+    usage = kernel_resources(r.stderr)
+    bad = [k for k, u in usage.items() if "k_solve_wide" in k and u.get("LDS Size [bytes/block]", 0) != 0]
+    if bad:
+        os.remove(LIB + ".tmp")
+        raise RuntimeError(f"static LDS in {bad}: the solver addresses its dynamic LDS from 0")
     os.replace(LIB + ".tmp", LIB)
     return LIB
+
+
+def kernel_resources(remarks: str) -> dict:
+    """Per-kernel resource usage from hipcc's kernel-resource-usage remarks
+    ({mangled name: {"VGPRs": .., "SGPRs Spill": .., "Occupancy [waves/SIMD]": .., ...}})."""
+    import re
+
+    out, cur = {}, None
+    for line in remarks.splitlines():
+        m = re.search(r"remark:\s+Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][^:]*?):\s+(-?\d+)", line)
+        if m and cur is not None:
+            cur[m.group(1).strip()] = int(m.group(2))
+    return out
 
 
 if __name__ == "__main__":
