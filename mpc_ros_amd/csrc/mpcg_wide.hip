@@ -1,7 +1,7 @@
 // mpc_ros_amd/csrc/mpcg_wide.hip -- one problem per wavefront (wide_core.h) on CDNA4.
 //
 // One workgroup = one wavefront = one problem; the problem's whole state lives in
-// the workgroup's LDS (WideLayout: 19.8 KB at N = 20, i.e. 8 problems resident per
+// the workgroup's LDS (WideLayout: 19.9 KB at N = 20, i.e. 8 problems resident per
 // CU).  Workgroups are dispatched by the hardware as CUs free up, so a slow problem
 // occupies one wavefront slot while the rest of the batch streams past it.
 #include <hip/hip_runtime.h>
