@@ -66,3 +66,26 @@ def test_shard_covers_exactly(total, world):
         seen.extend(range(s, s + c))
         assert c <= dist.max_shard(total, world)
     assert seen == list(range(total))
+
+
+def test_build_reads_kernel_resource_remarks():
+    """build.kernel_resources parses hipcc's kernel-resource-usage remarks; the build
+    refuses a solve kernel whose LDS is not all dynamic (static LDS would overlap the
+    solver's layout, which starts at address 0)."""
+    from mpc_ros_amd import build
+
+    text = "\n".join([
+        "x.hip:39:1: remark: Function Name: _ZN4mpcg12k_solve_wideILi0ELb1EdLi1ELb1EEEvNS_8WideArgsE [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:39:1: remark:     VGPRs: 256 [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:39:1: remark:     ScratchSize [bytes/lane]: 128 [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:39:1: remark:     Occupancy [waves/SIMD]: 2 [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:39:1: remark:     SGPRs Spill: 341 [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:39:1: remark:     LDS Size [bytes/block]: 4096 [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:80:1: remark: Function Name: _ZN4mpcg11k_sched_keyElPKdPfPi [-Rpass-analysis=kernel-resource-usage]",
+        "x.hip:80:1: remark:     VGPRs: 12 [-Rpass-analysis=kernel-resource-usage]",
+    ])
+    u = build.kernel_resources(text)
+    k = "_ZN4mpcg12k_solve_wideILi0ELb1EdLi1ELb1EEEvNS_8WideArgsE"
+    assert u[k] == {"VGPRs": 256, "ScratchSize [bytes/lane]": 128, "Occupancy [waves/SIMD]": 2,
+                    "SGPRs Spill": 341, "LDS Size [bytes/block]": 4096}
+    assert u["_ZN4mpcg11k_sched_keyElPKdPfPi"] == {"VGPRs": 12}
