@@ -14,7 +14,9 @@
  * outcomes are reported in `status` with CppAD::ipopt::solve_result::status_type
  * numbering (mpc_ros/include/cppad/ipopt/solve_result.hpp:30-46): 1 success,
  * 2 maxiter_exceeded, 3 stop_at_tiny_step, 4 stop_at_acceptable_point,
- * 9 restoration_failure, 10 error_in_step_computation, 11 invalid_number_detected,
+ * 5 local_infeasibility and 7 feasible_point_found (the feasibility-restoration phase
+ * converged without returning to the problem), 9 restoration_failure (the restoration
+ * phase's line search failed), 10 error_in_step_computation, 11 invalid_number_detected,
  * 14 unknown (Ipopt's CPUTIME_EXCEEDED, solve_callback.hpp:1165-1167: the max_cpu_time
  * budget below).  As in the reference (mpc_planner.cpp:378, the status is computed and
  * then ignored), the last iterate is always returned.
@@ -129,7 +131,9 @@ int mpcg_create(int device, mpcg_handle** out);
 void mpcg_destroy(mpcg_handle* h);
 int mpcg_set_params(mpcg_handle* h, const mpcg_params* p);
 int mpcg_get_params(const mpcg_handle* h, mpcg_params* p);
-/* Device workspace for B problems (bytes): the spill areas of the rare solver paths and the
+/* Device workspace for B problems (bytes): one slot per wavefront the GPU holds resident
+ * (not per problem: the rare solver paths' copies and the restoration phase's records), the
+ * park area of problems that enter the restoration phase (max(256, B/256) entries), and the
  * solve-order buffers; reserve it ahead of graph capture. */
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B);
 int mpcg_reserve(mpcg_handle* h, int64_t B);

@@ -71,12 +71,37 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         sys.stderr.write(r.stderr)
     usage = kernel_resources(r.stderr)
-    bad = [k for k, u in usage.items() if "k_solve_wide" in k and u.get("LDS Size [bytes/block]", 0) != 0]
+    bad = [k for k, u in usage.items() if ("k_solve_wide" in k or "k_resume_wide" in k) and u.get("LDS Size [bytes/block]", 0) != 0]
     if bad:
         os.remove(LIB + ".tmp")
         raise RuntimeError(f"static LDS in {bad}: the solver addresses its dynamic LDS from 0")
     os.replace(LIB + ".tmp", LIB)
+    save_resources(usage)
     return LIB
+
+
+RESOURCES = os.path.join(ROOT, "profiles", "r3", "resources.json")
+
+
+def demangle(names):
+    try:
+        out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")
+        return dict(zip(names, out))
+    except OSError:
+        return {n: n for n in names}
+
+
+def save_resources(usage: dict, path: str = RESOURCES) -> None:
+    """Register / spill / scratch / occupancy figures of every solver kernel instance and of the
+    restoration phase's out-of-line function, from the build's kernel-resource-usage remarks."""
+    import json
+
+    keep = {k: v for k, v in usage.items() if "k_solve_wide" in k or "k_resume_wide" in k or "resto_phase" in k}
+    names = demangle(sorted(keep))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump({"build_id": source_hash(), "arch": ARCH,
+                   "functions": {names[k]: keep[k] for k in sorted(keep)}}, f, indent=1)
 
 
 def kernel_resources(remarks: str) -> dict:

@@ -34,8 +34,10 @@
 
 #if defined(__HIPCC__)
 #define MPCG_HD __host__ __device__ __forceinline__
+#define MPCG_NOINLINE __host__ __device__ __attribute__((noinline))
 #else
 #define MPCG_HD inline
+#define MPCG_NOINLINE __attribute__((noinline))
 #endif
 namespace mpcg {
 
@@ -133,6 +135,8 @@ enum : int32_t {
     IPM_MAXITER = 2,
     IPM_TINY_STEP = 3,
     IPM_ACCEPTABLE = 4,
+    IPM_LOCAL_INFEASIBILITY = 5,  // the restoration phase converged to a point that is not feasible
+    IPM_FEASIBLE_POINT = 7,       // the restoration phase converged to a feasible point (FEASIBLE_POINT_FOUND)
     IPM_RESTORATION_FAILURE = 9,
     IPM_ERROR_IN_STEP = 10,
     IPM_INVALID_NUMBER = 11,

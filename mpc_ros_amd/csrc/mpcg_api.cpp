@@ -42,7 +42,7 @@ struct mpcg_handle {
     // solve-order buffers (keys, indices, sort scratch)
     void* d_sched = nullptr;
     size_t sched_bytes = 0;
-    // per-problem HBM spill areas of the solver's rare paths
+    // HBM workspace slots of the solver's rare paths and restoration phase (one per resident wavefront)
     double* d_spill = nullptr;
     size_t spill_bytes = 0;
     // stream ordering of the scratch above: the last stream that used it and an event
@@ -428,7 +428,8 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
         if (e != hipSuccess) return hip_fail(e, "solve-order sort");
         order = ord;
     }
-    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order, (void*)h->d_spill, s);
+    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order,
+                                (void*)h->d_spill, h->spill_bytes, s);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     return record_on(h, s);
 }

@@ -11,12 +11,14 @@ namespace mpcg {
 
 // One problem per wavefront (mpcg_wide.hip): LDS bytes per problem, launch.
 size_t wide_lds_bytes(const IpmParams& P);
-// HBM spill areas of B problems (watchdog, acceptable point, second-order corrections,
-// soft restoration: rare paths that must not cost LDS)
+// HBM workspace of a batch of B (watchdog, acceptable point, second-order corrections,
+// soft restoration, the restoration phase: rare paths that must not cost LDS): one slot
+// per wavefront the device holds resident (wide_slots), claimed by each problem's wavefront
 size_t wide_spill_bytes(const IpmParams& P, int64_t B);
+int64_t wide_slots(const IpmParams& P, int64_t B);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             void* spill, hipStream_t stream);
+                             void* spill, size_t spill_bytes, hipStream_t stream);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the
 // launch that writes the workgroup -> problem map into `buf` (returned in *order).
 size_t wide_sched_bytes(int64_t B);

@@ -24,8 +24,39 @@ struct WideArgs {
     int32_t* status;
     double* obj;
     int32_t* iters;
-    void* spill;           // per-problem HBM spill areas (WideLayout::spill() elements of T each)
+    void* slots;           // nslots workspaces of WideLayout::spill() elements of T (the rare paths' copies)
+    int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
+    int32_t nslots;
+    // parked problems (the restoration phase, continued by k_resume_wide): count, capacity,
+    // problem index and state of each
+    int32_t* park_count;
+    int32_t park_cap;
+    int64_t* park_idx;
+    void* park;
 };
+
+// A workspace slot for the wavefront's problem: the first free one from blockIdx mod
+// nslots on (nslots >= the resident wavefronts, so the first probe normally succeeds;
+// with fewer, a wavefront waits for a resident one to finish and release its slot).
+// Vector atomics through the L2 (device scope).
+__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int64_t hint) {
+    int s = (int)(hint % nslots);
+    int r = 0;
+    if (threadIdx.x == 0) {
+        for (;;) {
+            if (atomicCAS(&flags[s], 0, 1) == 0) break;
+            s = s + 1 == nslots ? 0 : s + 1;
+            if (s == (int)(hint % nslots)) __builtin_amdgcn_s_sleep(8);
+        }
+        r = s;
+    }
+    return __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+}
+__device__ __forceinline__ void release_slot(int32_t* flags, int s) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the slot's last stores before its release
+    __builtin_amdgcn_wave_barrier();
+    if (threadIdx.x == 0) atomicExch(&flags[s], 0);
+}
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
 // budget of 256 per lane lets all of them be resident
@@ -35,6 +66,9 @@ struct WideArgs {
 // NB: stage blocks (2 for 64 < N <= 128, lane t owning stages t and 64 + t).
 // DEFOPT: the Ipopt options are the reference's defaults (ipopt_default_options), compiled
 // as constants.
+template <class Solver>
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p);
+
 template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
@@ -50,8 +84,31 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
     const WideLayout Lw(Pk.N, Pk.filter_cap, MODEL);
-    WideSolver<DevWave, MODEL, SPLIT, T, NB> S(Pk, pr, wv, (T*)a.spill + p * (int64_t)Lw.spill());
+    const int slot = claim_slot(a.slot_flags, a.nslots, (int64_t)blockIdx.x);
+    typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
+    Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * Lw.spill());
     S.solve();
+    if (S.status == Solver::NEED_RESTO) {
+        // the restoration phase runs in k_resume_wide: park the problem
+        int e = 0;
+        if (t == 0) e = atomicAdd(a.park_count, 1);
+        e = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
+        if (e < a.park_cap) {
+            S.park((T*)a.park + (int64_t)e * Solver::park_elems(Lw));
+            if (t == 0) a.park_idx[e] = p;
+            release_slot(a.slot_flags, slot);
+            return;
+        }
+        S.status = IPM_RESTORATION_FAILURE;  // (more parked problems than the park area holds)
+    }
+    write_out(a, S, p);
+    release_slot(a.slot_flags, slot);
+}
+
+// results of problem p (u0, status, iterations, objective, trajectory; honor_original_bounds)
+template <class Solver>
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p) {
+    const int t = threadIdx.x;
     const double o = (double)S.objective_out();
     const int N = a.P.N;
     if (t == 0) {
@@ -69,6 +126,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
             tr[2 * N + k] = (double)S.x_state(2, k);
         }
     }
+}
+
+// The parked problems: the restoration phase (WideSolver<..., RESTO> out of line) and the
+// rest of the solve, from the state k_solve_wide parked -- the same solver instance, so the
+// iterates are those the first kernel would have continued with.  A separate kernel keeps
+// the call out of the batch kernel's register allocation; it runs over the park area only.
+template <int MODEL, bool SPLIT, class T, int NB>
+__global__ void __launch_bounds__(64) k_resume_wide(WideArgs a) {
+    const int n = *a.park_count < a.park_cap ? *a.park_count : a.park_cap;
+    const int e = (int)blockIdx.x;
+    if (e >= n) return;
+    const int64_t p = a.park_idx[e];
+    const int t = threadIdx.x;
+    IpmProblem<T> pr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
+    DevWave wv;
+    wv.t = t;
+    const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
+    typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
+    T* ent = (T*)a.park + (int64_t)e * Solver::park_elems(Lw);
+    Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
+    S.unpark(ent);
+    S.finish_resto();
+    write_out(a, S, p);
 }
 
 // Scheduling key: workgroups are dispatched roughly in index order, so a slow problem
@@ -113,34 +197,86 @@ static size_t elem_bytes(const IpmParams& P) { return P.precision == 1 ? sizeof(
 size_t wide_lds_bytes(const IpmParams& P) {
     return (size_t)WideLayout(P.N, P.filter_cap, P.model).total() * elem_bytes(P);
 }
+
+// the resume kernel of a solve kernel's instance (the general-options instance also for the
+// default-options one: the two compute bitwise the same)
+static const void* resume_kernel(const IpmParams& P) {
+    const bool split = P.N <= 32;
+    const bool f32 = P.precision == 1;
+    const int nb = P.N > 64 ? 2 : 1;
+    if (P.N > 128 || (f32 && P.model != 0)) return nullptr;
+    if (f32)
+        return nb == 2 ? (const void*)k_resume_wide<0, false, float, 2>
+             : split ? (const void*)k_resume_wide<0, true, float, 1> : (const void*)k_resume_wide<0, false, float, 1>;
+    if (P.model == 1)
+        return nb == 2 ? (const void*)k_resume_wide<1, false, double, 2>
+             : split ? (const void*)k_resume_wide<1, true, double, 1> : (const void*)k_resume_wide<1, false, double, 1>;
+    return nb == 2 ? (const void*)k_resume_wide<0, false, double, 2>
+         : split ? (const void*)k_resume_wide<0, true, double, 1> : (const void*)k_resume_wide<0, false, double, 1>;
+}
+
+// (model, split, precision, blocks, default options) -> kernel instance; null if none
+static const void* wide_kernel(const IpmParams& P) {
+    const bool split = P.N <= 32;
+    const bool f32 = P.precision == 1;
+    const int nb = P.N > 64 ? 2 : 1;
+    if (P.N > 128) return nullptr;
+    if (f32 && P.model != 0) return nullptr;  // (fp32: the differential drive)
+    if (f32)
+        return nb == 2 ? (const void*)k_solve_wide<0, false, float, 2>
+             : split ? (const void*)k_solve_wide<0, true, float, 1> : (const void*)k_solve_wide<0, false, float, 1>;
+    if (P.model == 1)
+        return nb == 2 ? (const void*)k_solve_wide<1, false, double, 2>
+             : split ? (const void*)k_solve_wide<1, true, double, 1> : (const void*)k_solve_wide<1, false, double, 1>;
+    if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
+        return (const void*)k_solve_wide<0, true, double, 1, true>;
+    return nb == 2 ? (const void*)k_solve_wide<0, false, double, 2>
+         : split ? (const void*)k_solve_wide<0, true, double, 1> : (const void*)k_solve_wide<0, false, double, 1>;
+}
+
+// Workspace slots for a batch of B: four times the wavefronts the device can hold resident at
+// once (occupancy of the instance at its LDS size times the CUs), at most B.  A wavefront
+// claims slot blockIdx mod nslots, or the next free one: with the margin, a slow problem
+// still holding a slot rarely makes a later wavefront probe further.
+int64_t wide_slots(const IpmParams& P, int64_t B) {
+    if (B <= 0) return 0;
+    int64_t n = 4096;  // (fallback if the runtime cannot say)
+    const void* fn = wide_kernel(P);
+    int dev = 0, cus = 0, per = 0;
+    if (fn && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds_bytes(P)) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64, wide_lds_bytes(P)) == hipSuccess && per > 0 &&
+        cus > 0)
+        n = 4 * (int64_t)per * cus;
+    return n < B ? n : B;
+}
+static size_t slot_flag_bytes(int64_t nslots) { return ((size_t)nslots * sizeof(int32_t) + 255) & ~(size_t)255; }
+// the park area: problems that enter the restoration phase (rare: ~5e-5 of the infinity set at
+// N = 20, 5e-4 at N = 40); beyond its capacity a problem ends with restoration_failure
+int64_t wide_park_cap(int64_t B) {
+    const int64_t c = B / 256 > 256 ? B / 256 : 256;
+    return c < B ? c : B;
+}
+static size_t park_elems(const IpmParams& P) {
+    const WideLayout L(P.N, P.filter_cap, P.model);
+    return (size_t)(32 + L.total() + L.slot());  // (WideSolver::park_elems)
+}
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
-    return (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)B;
+    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
+    return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) +
+           (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns +
+           park_elems(P) * elem_bytes(P) * (size_t)pc;
 }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             void* spill, hipStream_t stream) {
+                             void* spill, size_t spill_bytes, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
-    const bool split = P.N <= 32;
-    const bool f32 = P.precision == 1;
-    const int nb = P.N > 64 ? 2 : 1;
-    if (P.N > 128) return hipErrorInvalidValue;
-    if (f32 && P.model != 0) return hipErrorInvalidValue;  // (fp32: the differential drive)
-    // (model, split, precision, blocks) -> instantiation
-    const void* fn;
-    if (f32)
-        fn = nb == 2 ? (const void*)k_solve_wide<0, false, float, 2>
-           : split ? (const void*)k_solve_wide<0, true, float, 1> : (const void*)k_solve_wide<0, false, float, 1>;
-    else if (P.model == 1)
-        fn = nb == 2 ? (const void*)k_solve_wide<1, false, double, 2>
-           : split ? (const void*)k_solve_wide<1, true, double, 1> : (const void*)k_solve_wide<1, false, double, 1>;
-    else if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
-        fn = (const void*)k_solve_wide<0, true, double, 1, true>;
-    else
-        fn = nb == 2 ? (const void*)k_solve_wide<0, false, double, 2>
-           : split ? (const void*)k_solve_wide<0, true, double, 1> : (const void*)k_solve_wide<0, false, double, 1>;
+    const void* fn = wide_kernel(P);
+    if (!fn) return hipErrorInvalidValue;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -148,9 +284,34 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, spill};
+    // the workspace (wide_spill_bytes): slot flags | park count (256 B) | park indices | slots | park area
+    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
+    if (ns < 1 || wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
+    char* w = (char*)spill;
+    int32_t* flags = (int32_t*)w;
+    w += slot_flag_bytes(ns);
+    int32_t* pcount = (int32_t*)w;
+    w += 256;
+    int64_t* pidx = (int64_t*)w;
+    w += (size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255;
+    void* slots = w;
+    w += (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns;
+    void* park = w;
+    e = hipMemsetAsync(spill, 0, slot_flag_bytes(ns) + 256, stream);  // (flags and the park count)
+    if (e != hipSuccess) return e;
+    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, slots, flags, (int32_t)ns,
+                     pcount, (int32_t)pc, pidx, park};
     void* args[] = {(void*)&a};
     e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
+    if (e != hipSuccess) return e;
+    // the parked problems (a grid over the park area; workgroups beyond the count exit at once)
+    const void* rf = resume_kernel(P);
+    e = hipFuncGetAttributes(&fa, rf);
+    if (e != hipSuccess) return e;
+    if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+    e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

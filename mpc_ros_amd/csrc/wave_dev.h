@@ -56,6 +56,14 @@ struct DevWaveBase {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    // order global-memory accesses across the lanes of the wavefront (the restoration
+    // phase's HBM records written by one lane and read by another): workgroup-scope release
+    // and acquire -- the vector memory operations of a workgroup share the CU's L1
+    __device__ __forceinline__ void gsync() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
     __device__ __forceinline__ void ld2(int i, double& a, double& b) const {
         const double2 v = *(const ldsT2*)(S() + i);
         a = v.x;
@@ -181,6 +189,14 @@ struct DevWaveBase {
     __device__ __forceinline__ double lane0(double v) const {
         return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 0),
                                 __builtin_amdgcn_readlane(__double2loint(v), 0));
+    }
+    // the value of lane l (l wave-uniform)
+    __device__ __forceinline__ double lanev(double v, int l) const {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                                __builtin_amdgcn_readlane(__double2loint(v), l));
+    }
+    __device__ __forceinline__ float lanev(float v, int l) const {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
     }
     __device__ __forceinline__ float lane63(float v) const {
         return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));

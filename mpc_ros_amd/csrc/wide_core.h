@@ -85,7 +85,8 @@ struct WideLayout {
     MPCG_HD int PRB() const { return CTL() + 16; }
     MPCG_HD int PRC() const { return PRB() + 6; }
     MPCG_HD int total() const { return PRB() + 12; }
-    // Per-problem HBM spill area (doubles) of the rare paths: the watchdog's stored iterate
+    // Per-wavefront HBM workspace (elements of T) of the rare paths, one per resident
+    // wavefront (mpcg_wide.hip claims a slot per problem).  The watchdog's stored iterate
     // and direction (LDS [W(0), YP(N)) = 52N), the last acceptable iterate (W: 10N), the
     // Newton direction kept while second-order corrections are tried (DW, YP: 16N), the
     // iterate kept while a soft-restoration step is evaluated (W, ZL, ZU, Y: 36N).
@@ -94,7 +95,43 @@ struct WideLayout {
     MPCG_HD int SP_SOC() const { return 62 * N; }
     MPCG_HD int SP_SOFT() const { return 78 * N; }
     MPCG_HD int spill() const { return 114 * N; }
+    // The feasibility-restoration phase (WideSolver<..., RESTO = true>, entered from the
+    // original problem's line search): the original problem's LDS image while the
+    // restoration problem uses the LDS (total()), the restoration problem's per-stage
+    // records of the penalty variables p, n of the rows into stage k (XS), and their copies
+    // for the watchdog / second-order corrections / soft restoration (XSP).  The
+    // restoration problem's own LDS-part copies reuse SP_WD, SP_SOC and SP_SOFT (the
+    // original's SP_ACC is kept).
+    static constexpr int XP = 0, XN = 6, XZP = 12, XZN = 18, XDP = 24, XDN = 30;  // p, n, z_p, z_n, dp, dn
+    static constexpr int XCR = 36;  // constraint right-hand side of the rows (scaled): c(x) - p + n, or a SOC's
+    static constexpr int XDS = 42;  // sqrt of the rows' diagonal D (unscaled rows) in the reduced system
+    static constexpr int XM = 48;    // soft rows: ds_k = M z + m (M 6x6 row-major on the states) ...
+    static constexpr int XMN = 84;   // ... their slack e = ds_k - z = N z + m, N = M - I (6x6) ...
+    static constexpr int XMV = 120;  // ... m
+    static constexpr int XE = 126;   // e of the last step (row form)
+    static constexpr int XS = 132;
+    static constexpr int XW = 72;   // spill copies: watchdog p n zp zn dp dn (0..35), SOC dp dn (36..47), soft p n zp zn (48..71)
+    MPCG_HD int SP_DUMP() const { return spill(); }
+    MPCG_HD int SP_EXT() const { return spill() + total(); }
+    MPCG_HD int SP_XSP() const { return SP_EXT() + XS * N; }
+    MPCG_HD int slot() const { return SP_XSP() + XW * N; }
 };
+
+// The original problem's values the restoration phase needs (passed by value into its
+// out-of-line function) and its result.
+template <class T>
+struct RestoIn {
+    T mu, tau, theta, prim_inf, ref_phi, ref_theta, sf;
+    int nf, iter;
+};
+struct RestoOut {
+    int status;  // 0: the restoration phase found a point the original problem accepts
+    int iter;
+};
+// The restoration phase of the problem whose wavefront state is in LDS and whose workspace
+// slot is ws (defined after WideSolver; out of line).
+template <class WV, int MODEL, class T, int NB>
+MPCG_NOINLINE RestoOut resto_phase(const IpmParams& P, IpmProblem<T> pr, WV wv, T* ws, RestoIn<T> in);
 
 // MODEL: 0 differential drive (FG_eval), 1 kinematic bicycle -- a template parameter
 // so that the differential-drive kernel carries none of the bicycle's terms.
@@ -107,9 +144,21 @@ struct WideLayout {
 // NB: stage blocks -- 1 for N <= 64 (lane t owns stage t), 2 for 64 < N <= 128 (lane t owns
 // stages t and 64 + t: the stage-parallel sweeps loop over the blocks, the dynamics of
 // stage 63 reach stage 64 by a lane read, the systolic recursions run block by block).
-template <class WV, int MODEL = 0, bool SPLIT = false, class TT = double, int NB = 1>
+// RESTO: the instance that solves Ipopt's feasibility-restoration problem (RestoIpoptNLP,
+// oracle/ipm.c perform_restoration) from the original problem's iterate:
+//   min rho sum(p + n) + eta(mu)/2 ||D_R (x - x_R)||^2,  eta = sqrt(mu), D_R = diag(1/max(1,|x_R|))
+//   s.t. c(x) - p + n = 0 (c: the original's scaled rows), x in the original's bounds, p, n >= 0.
+// Its Newton system eliminates p and n (Ipopt's AugRestoSystemSolver): the dynamics rows
+// become soft, J dx - D y+ = -c_hat with a positive diagonal D, and the Riccati recursion
+// absorbs each row block by the update P~ = P - P D^1/2 S^-1 D^1/2 P, S = I + D^1/2 P D^1/2
+// (the inertia test adds: every S positive definite).  Unsplit sweeps only (SPLIT = false),
+// block loops for any N <= 128.  A separate instantiation, called out of line from the
+// original problem's line search (resto_phase below): the main kernel's register
+// allocation does not see it.
+template <class WV, int MODEL = 0, bool SPLIT = false, class TT = double, int NB = 1, bool RESTO = false>
 struct WideSolver {
     static_assert(NB == 1 || !SPLIT, "the half-wave split is for N <= 32");
+    static_assert(!RESTO || !SPLIT, "the restoration problem runs the unsplit sweeps");
     typedef TT T;
     static constexpr double EPS = sizeof(TT) == 4 ? 1.1920928955078125e-07 : 2.220446049250313e-16;
     const IpmParams P;
@@ -180,6 +229,25 @@ struct WideSolver {
 #endif
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
+
+    // ---- the restoration problem (RESTO instance only; oracle/ipm.c perform_restoration)
+    static constexpr double RHO = 1000.0;  // resto_penalty_parameter
+    static constexpr double KD = 1e-5;     // kappa_d: the barrier's damping of one-sided bounds (p, n >= 0)
+    enum : int { RESTO_DONE = 100 };       // the original problem accepts the restoration iterate
+    enum : int { NEED_RESTO = 101 };       // the original problem enters the restoration phase
+    T* ext = nullptr;                      // HBM records of the rows into each stage (WideLayout::XS)
+    T* xsp = nullptr;                      // HBM copies of the records (WideLayout::XW)
+    T* dumpO = nullptr;                    // the original problem's LDS image: x_R = its iterate, its filter
+    T o_mu = 0, o_tau = 0, o_theta = 0, o_ref_phi = 0, o_ref_theta = 0, o_sf = 1;
+    int o_nf = 0;
+    bool resto_first = false;
+    // statistics of the restoration iterate: sum(p + n), ||D_R (x - x_R)||^2, and the original
+    // problem's barrier function, violation and max violation at x
+    T r_spn = 0, r_qx = 0, r_phiO = 0, r_thO = 0, r_pinfO = 0;
+    // the monotone barrier update's loop state across a re-evaluation (k_rmu)
+    T mu_Emu = 0;
+    int mu_tf = 0;
+    bool mu_done = false;
 
     MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_, T* spill_)
         : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf),
@@ -460,8 +528,33 @@ struct WideSolver {
                     st(L.Y(k) + j, y + alpha * (yp - y));
                 }
             }
+            if constexpr (RESTO) accept_rows(t, alpha, amax_z, clamp);
         }
         wv.sync();
+    }
+    // (RESTO) the rows' p, n and their bound multipliers: lane t owns the rows into stages t
+    // (and 64 + t) -- their HBM records are read and written by that lane only
+    MPCG_HD void accept_rows(int t, T alpha, T amax_z, bool clamp) {
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int ov = h ? WideLayout::XN : WideLayout::XP, oz = h ? WideLayout::XZN : WideLayout::XZP;
+                    const int od = h ? WideLayout::XDN : WideLayout::XDP;
+                    const T v = x[ov + j], z = x[oz + j], dv = x[od + j];
+                    const T dz = mu / v - z - z / v * dv;
+                    const T vn = v + alpha * dv;
+                    T zn = z + amax_z * dz;
+                    if (clamp) zn = tmax(tmin(zn, (T)1e10 * mu / vn), mu / ((T)1e10 * vn));
+                    x[ov + j] = vn;
+                    x[oz + j] = zn;
+                }
+            }
+        }
     }
 
     // Statistics of the iterate (SPLIT): lane k of the lower half-wave takes stage k's
@@ -641,6 +734,10 @@ struct WideSolver {
     }
 
     MPCG_HD void stats(bool acc, T alpha, T amax_z) {
+        if constexpr (RESTO) {
+            stats_resto(acc, alpha, amax_z);
+            return;
+        }
         if constexpr (SPLIT) {
             stats_split(acc, alpha, amax_z);
             return;
@@ -1068,6 +1165,12 @@ struct WideSolver {
     }
 
     MPCG_HD void precompute(int mode, T delta_w) {
+        if constexpr (RESTO) {
+            const int t = wv.lane();
+            for (int b = 0; b < NB; ++b) precompute_resto(t + 64 * b, delta_w);
+            wv.gsync();  // (the rows' D, written to HBM per stage, are read by every lane of the Riccati sweep)
+            return;
+        }
         if constexpr (SPLIT) {
             precompute_split(mode, delta_w);
             return;
@@ -1202,7 +1305,9 @@ struct WideSolver {
         // control's columns, the same for every stage (the Newton system, mode 0).  Stage 0
         // has no previous control: its coupling entries act only on K_0's columns 6, 7, which
         // multiply a zero step, and on P_0, which is not used.
-        const T C0 = mode == 0 ? -sf * (T)(2.0 * P.w_dw) : (T)0, C1 = mode == 0 ? -sf * (T)(2.0 * P.w_da) : (T)0;
+        // (the restoration problem's Hessian has no objective terms: no rate coupling)
+        const T C0 = (mode == 0 && !RESTO) ? -sf * (T)(2.0 * P.w_dw) : (T)0;
+        const T C1 = (mode == 0 && !RESTO) ? -sf * (T)(2.0 * P.w_da) : (T)0;
         const T cc0j = j == 6 ? C0 : (T)0, cc1j = j == 7 ? C1 : (T)0;
         const T cc0i = i == 6 ? C0 : (T)0, cc1i = i == 7 ? C1 : (T)0;
         // the gains' store at ga0 + gak * k: lanes 0..15 K[0][j], K[1][j], lanes 16, 17 k;
@@ -1234,6 +1339,8 @@ struct WideSolver {
         }
         bool bad = false;  // a stage's reduced Hessian not positive definite
         for (int k = N - 2; k >= 0; --k) {
+            // (RESTO) the soft rows into stage k + 1 absorbed into its cost-to-go first
+            if constexpr (RESTO) soft_rows(k + 1, Pij, pvi, bad);
             const int sb = L.ST(k);
             // row i of P' (16-byte reads of the scratch the previous stage wrote) and all
             // P-independent stage data, issued together before anything waits on them
@@ -1319,6 +1426,10 @@ struct WideSolver {
             st(ga0 + gak * k, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
             st(sm + MS * i + j, gnext);
         }
+        if constexpr (RESTO) {
+            soft_rows(0, Pij, pvi, bad);  // the initial-state rows (soft as well)
+            wv.gsync();                   // (the gains M, m in HBM are read by other lanes in forward())
+        }
         // a failed inertia test anywhere (the stages after it computed values the retry overwrites)
         if (wv.uni(bad)) {
             wv.mark(2);
@@ -1396,6 +1507,7 @@ struct WideSolver {
     }
 
     MPCG_HD Fwd forward(int mode) {
+        if constexpr (RESTO) return forward_resto();
         if constexpr (NB == 2) return forward_blk(mode);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
         wv.sync();
@@ -1866,6 +1978,7 @@ struct WideSolver {
     }
 
     MPCG_HD bool trial(T alpha, T* phi, T* th) {
+        if constexpr (RESTO) return trial_resto(alpha, phi, th);
         if constexpr (SPLIT) return trial_split(alpha, phi, th);
         if constexpr (NB == 2) return trial_blk(alpha, phi, th);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
@@ -1924,6 +2037,802 @@ struct WideSolver {
         *phi = sf * f - mu * lg;
         *th = thv;
         return !anybad && isfinite((double)*phi);
+    }
+
+    // ------------------------------------------------------------ the restoration problem's sweeps
+    // (RESTO instance.)  x = the stage variables in LDS as in the original problem; the rows'
+    // p, n, z_p, z_n and steps in HBM records owned by the lane of the stage the rows lead into.
+    MPCG_HD T* xrec(int k) const { return ext + (size_t)k * WideLayout::XS; }
+    MPCG_HD T xR(int k, int j) const { return dumpO[L.W(k) + j]; }  // the reference point x_R
+    MPCG_HD T dR(int k, int j) const { return (T)1 / tmax((T)1, (T)fabs(xR(k, j))); }
+    MPCG_HD T eta_mu() const { return (T)sqrt((double)mu); }  // resto_proximity_weight 1 * sqrt(mu)
+    // the barrier function of the current iterate (kappa_d damping of p, n)
+    MPCG_HD T phi_cur() const {
+        if constexpr (RESTO) return wv.uni_d(fval - mu * logsum + (T)KD * mu * r_spn);
+        return wv.uni_d(sf * fval - mu * logsum);
+    }
+    // the original problem's scaled rows into the lane's stages at the stage variables w
+    // (c = rsc (s_k - F(s_{k-1}, u_{k-1})), rows 0: s_0 - init)
+    MPCG_HD void rows_c(const T (&w)[NB][8], T (&cs)[NB][6]) {
+        const int t = wv.lane();
+        T Fk[NB][6], Fprev[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) Fk[b][j] = 0;
+            if (k < N - 1) {
+                Lin<T> ln;
+                ln.eval(pcoef().c, w[b]);
+                next_m(ln, w[b], w[b] + 6, Fk[b]);
+            }
+        }
+        shift_blocks(Fk, Fprev);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T c = k == 0 ? w[b][j] - pinit(j) : w[b][j] - Fprev[b][j];
+                cs[b][j] = k < N ? rowscale(j, k) * c : (T)0;
+            }
+        }
+    }
+    MPCG_HD void load_w(T (&w)[NB][8], T alpha, bool step) const {
+        const int t = wv.lane();
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[b][j] = 0;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < nv) w[b][j] = step ? ld(L.W(k) + j) + alpha * ld(L.DW(k) + j) : ld(L.W(k) + j);
+        }
+    }
+
+    // RestoIterateInitializer: x = the original iterate, its bound multipliers capped at rho,
+    // p and n the minimisers of the penalty with barrier mu_R for fixed x, z_p = mu_R / p,
+    // z_n = mu_R / n, y = 0
+    MPCG_HD void init_rows() {
+        const int t = wv.lane();
+        wv.sync();
+        T w[NB][8], cs[NB][6];
+        load_w(w, (T)0, false);
+        rows_c(w, cs);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    st(L.ZL(k) + j, tmin((T)RHO, ld(L.ZL(k) + j)));
+                    st(L.ZU(k) + j, tmin((T)RHO, ld(L.ZU(k) + j)));
+                }
+            }
+            T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                st(L.Y(k) + j, 0);
+                const T c = cs[b][j];
+                const T a = mu / ((T)2 * (T)RHO) - (T)0.5 * c, bb = c * mu / ((T)2 * (T)RHO);
+                const T nn = a + (T)sqrt((double)(a * a + bb)), pp = c + nn;
+                x[WideLayout::XP + j] = pp;
+                x[WideLayout::XN + j] = nn;
+                x[WideLayout::XZP + j] = mu / pp;
+                x[WideLayout::XZN + j] = mu / nn;
+                x[WideLayout::XDP + j] = 0;
+                x[WideLayout::XDN + j] = 0;
+            }
+        }
+        wv.sync();
+    }
+
+    // Statistics of the restoration iterate (eval_current on RestoIpoptNLP), with the stage
+    // data of its Newton system (A_k, curvature) and the rows' right-hand side c(x) - p + n.
+    MPCG_HD void stats_resto(bool acc, T alpha, T amax_z) {
+        const int t = wv.lane();
+        accept_all(t, acc, alpha, amax_z);
+        const T eta = eta_mu();
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], yn[6] = {0, 0, 0, 0, 0, 0}, a[7] = {0, 0, 0, 0, 0, 0, 0}, cvk[5] = {0, 0, 0, 0, 0};
+            T twk = dt, tvk = 0, hvdk = 0;
+            ldn<8>(L.W(k), w);
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                Lin<T> ln;
+                ln.eval(pcoef().c, w);
+                ln.jac(w, dt, a);
+                turn_d(w, w + 6, &twk, &tvk);
+                if (model == 1) hvdk = -(yn[2] + yn[5]) / lf * dt;
+                const T v = w[3];
+                cvk[0] = -yn[4] * ln.f2;
+                cvk[1] = yn[0] * v * ln.ct * dt + yn[1] * v * ln.st * dt;
+                cvk[2] = yn[0] * ln.st * dt - yn[1] * ln.ct * dt;
+                cvk[3] = yn[4] * v * ln.se * dt;
+                cvk[4] = -yn[4] * ln.ce * dt;
+            }
+            const int sb = L.ST(k);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) st(sb + WideLayout::SA + j, a[j]);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) st(sb + WideLayout::SCV + j, cvk[j]);
+            if constexpr (MODEL == 1) {
+                st(sb + WideLayout::STW, twk);
+                st(sb + WideLayout::STV, tvk);
+                st(sb + WideLayout::SHVD, hvdk);
+            }
+        }
+        T wv8[NB][8], cs[NB][6];
+        load_w(wv8, (T)0, false);
+        rows_c(wv8, cs);
+        T fO = 0, th = 0, pinf = 0, dinf = 0, c0 = 0, mn = (T)INFINITY, mx = -(T)INFINITY, ly = 0, lz = 0, lgx = 0,
+          lgpn = 0, spn = 0, qx = 0, thO = 0, pinfO = 0;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, up[2] = {0, 0}, um[2] = {0, 0}, a[8];
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            ldn<7>(L.ST(k) + WideLayout::SA, a);
+            T twk = dt, tvk = 0;
+            if constexpr (MODEL == 1) {
+                twk = ld(L.ST(k) + WideLayout::STW);
+                tvk = ld(L.ST(k) + WideLayout::STV);
+            }
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                up[0] = ld(L.W(k + 1) + 6);
+                up[1] = ld(L.W(k + 1) + 7);
+            }
+            if (k >= 1) {
+                um[0] = ld(L.W(k - 1) + 6);
+                um[1] = ld(L.W(k - 1) + 7);
+            }
+            T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+                const T zp = x[WideLayout::XZP + j], zn = x[WideLayout::XZN + j];
+                const T c = cs[b][j], cr = c - p + n;
+                x[WideLayout::XCR + j] = cr;
+                th += fabs(cr);
+                pinf = tmax(pinf, (T)fabs(cr));
+                thO += fabs(c);
+                pinfO = tmax(pinfO, (T)fabs(c));
+                const T ys = y[j] * rcp(rowscale(j, k));
+                ly += fabs(ys);
+                const T rdp = (T)RHO - ys - zp, rdn = (T)RHO + ys - zn;
+                dinf = tmax(dinf, tmax((T)fabs(rdp), (T)fabs(rdn)));
+                const T pp = p * zp, qq = n * zn;
+                c0 = tmax(c0, tmax((T)fabs(pp), (T)fabs(qq)));
+                mn = tmin(mn, tmin(pp, qq));
+                mx = tmax(mx, tmax(pp, qq));
+                lz += fabs(zp) + fabs(zn);
+                lgpn += log(p * n);
+                spn += p + n;
+            }
+            fO += cost_state(w);
+            T at[6] = {0, 0, 0, 0, 0, 0};
+            if (!last) {
+                AT_mul(a, yn, at);
+                if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
+                fO += cost_ctrl(k, w + 6, up);
+            }
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dr = dR(k, j), dxr = w[j] - xR(k, j);
+                    const T gq = eta * dr * dr * dxr;
+                    qx += (dr * dxr) * (dr * dxr);
+                    const T gj = j < 6 ? gq + y[j] - at[j] : gq - (j == 6 ? btw : bta);
+                    dinf = tmax(dinf, (T)fabs(gj - zl[j] + zu[j]));
+                    const T dl = w[j] - vlo(j), du = vhi(j) - w[j];
+                    slackprod *= dl * du;
+                    const T p1 = dl * zl[j], p2 = du * zu[j];
+                    c0 = tmax(c0, tmax((T)fabs(p1), (T)fabs(p2)));
+                    mn = tmin(mn, tmin(p1, p2));
+                    mx = tmax(mx, tmax(p1, p2));
+                    lz += fabs(zl[j]) + fabs(zu[j]);
+                }
+            }
+            lgx += log(slackprod);
+        }
+        T v[15] = {fO, th, pinf, dinf, c0, mn, mx, ly, lz, lgx, lgpn, spn, qx, thO, pinfO};
+        const int op[15] = {RSUM, RSUM, RMAX, RMAX, RMAX, RMIN, RMAX, RSUM, RSUM, RSUM, RSUM, RSUM, RSUM, RSUM, RMAX};
+        reduce<15, true>(v, op);
+        r_spn = v[11];
+        r_qx = v[12];
+        fval = wv.uni_d((T)RHO * r_spn + (T)0.5 * eta * r_qx);
+        theta = v[1];
+        prim_inf = v[2];
+        prim_uns = v[2];
+        dual_inf = v[3];
+        compl0 = v[4];
+        pmin = v[5];
+        pmax = v[6];
+        l1y = v[7];
+        l1z = v[8];
+        logsum = wv.uni_d(v[9] + v[10]);
+        // barrier_phi of the original problem at x (its mu; no one-sided bounds)
+        r_phiO = wv.uni_d(o_sf * v[0] - o_mu * v[9]);
+        r_thO = v[13];
+        r_pinfO = v[14];
+        wv.mark(0);
+    }
+
+    // the restoration problem's barrier function and violation at w + alpha dw, (p, n) + alpha (dp, dn)
+    MPCG_HD bool trial_resto(T alpha, T* phi, T* th) {
+        const int t = wv.lane();
+        const T eta = eta_mu();
+        T w[NB][8], cs[NB][6];
+        load_w(w, alpha, true);
+        rows_c(w, cs);
+        T qx = 0, thv = 0, lg = 0, spn = 0;
+        int bad = 0;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+            T slackprod = 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dl = w[b][j] - vlo(j), du = vhi(j) - w[b][j];
+                    bad |= !((dl > 0) && (du > 0));
+                    slackprod *= dl * du;
+                    const T d = dR(k, j) * (w[b][j] - xR(k, j));
+                    qx += d * d;
+                }
+            }
+            lg += log(slackprod);
+            const T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T p = x[WideLayout::XP + j] + alpha * x[WideLayout::XDP + j];
+                const T n = x[WideLayout::XN + j] + alpha * x[WideLayout::XDN + j];
+                bad |= !((p > 0) && (n > 0));
+                lg += log(p * n);
+                spn += p + n;
+                thv += fabs(cs[b][j] - p + n);
+            }
+        }
+        T v[4] = {qx, thv, lg, spn};
+        const int op[4] = {RSUM, RSUM, RSUM, RSUM};
+        reduce<4, true>(v, op);
+        const bool anybad = wv.any(bad != 0);
+        *phi = wv.uni_d((T)RHO * v[3] + (T)0.5 * eta * v[0] - mu * v[2] + (T)KD * mu * v[3]);
+        *th = v[1];
+        return !anybad && isfinite((double)*phi);
+    }
+
+    // Stage data of the reduced Newton system: x's barrier Hessian diagonal and gradient
+    // (no objective curvature: eta D_R^2 on the diagonal), and the rows' elimination of p, n
+    // (AugRestoSystemSolver): D = 1/(Sigma_p + dw) + 1/(Sigma_n + dw),
+    // c_hat = c_R + r_p/(Sigma_p + dw) - r_n/(Sigma_n + dw) + D y (scaled rows), in row form
+    // D / rsc^2 and c_hat / rsc; -c_hat is the defect of the step recursion (SD, C0).
+    MPCG_HD void precompute_resto(int k, T delta_w) {
+        if (k >= N) return;
+        const bool last = k == N - 1;
+        const int sb = L.ST(k);
+        const T eta = eta_mu();
+        T w[8], zl[8], zu[8];
+        ldn<8>(L.W(k), w);
+        ldn<8>(L.ZL(k), zl);
+        ldn<8>(L.ZU(k), zu);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            T qd = 0, qv = 0;
+            if (j < 6 || !last) {
+                const T dr = dR(k, j);
+                const T rdl = (T)1 / (w[j] - vlo(j)), rdu = (T)1 / (vhi(j) - w[j]);
+                qd = eta * dr * dr + zl[j] * rdl + zu[j] * rdu + delta_w;
+                qv = eta * dr * dr * (w[j] - xR(k, j)) - mu * rdl + mu * rdu;
+            }
+            st(sb + WideLayout::SQD + j, qd);
+            st(sb + WideLayout::SQV + j, qv);
+        }
+        T* x = xrec(k);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const T rsc = rowscale(j, k);
+            const T ys = ld(L.Y(k) + j) * rcp(rsc);
+            const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+            const T sp_ = x[WideLayout::XZP + j] / p + delta_w, sn_ = x[WideLayout::XZN + j] / n + delta_w;
+            // (c_hat = c + r_p/sp - r_n/sn + D y = c + gphi_p/sp - gphi_n/sn: the y terms
+            // cancel exactly, and are left out -- large where a row is active)
+            (void)ys;
+            const T gp = (T)RHO - mu / p + (T)KD * mu, gn = (T)RHO - mu / n + (T)KD * mu;
+            const T D = (T)1 / sp_ + (T)1 / sn_;
+            const T ch = x[WideLayout::XCR + j] + gp / sp_ - gn / sn_;
+            x[WideLayout::XDS + j] = (T)sqrt((double)(D / (rsc * rsc)));
+            const T dbar = -ch / rsc;
+            if (k == 0)
+                st(L.C0() + j, dbar);
+            else
+                st(L.ST(k - 1) + WideLayout::SD + j, dbar);
+        }
+    }
+
+    // The rows into stage kk absorbed into its cost-to-go (P, p of the lane's entry (i, j),
+    // row-major P in the scratch): S = I + D^1/2 P_ss D^1/2 (LDL^T, every pivot > 0 or the
+    // inertia test fails), P~ = P - P D^1/2 S^-1 D^1/2 P, p~ = p - P D^1/2 S^-1 D^1/2 p,
+    // and the gains of the step recursion ds = M z + m, M = I - D^1/2 S^-1 D^1/2 P,
+    // m = -D^1/2 S^-1 D^1/2 p (z: the state the hard dynamics would give).  Every lane
+    // factors S (the same values); lane (i, j) solves for its column j.
+    MPCG_HD void soft_rows(int kk, T& Pij, T& pvi, bool& bad) {
+        const int t = wv.lane();
+        const int i = t >> 3, j = t & 7;
+        const int sp = L.PSC();
+        T* x = xrec(kk);
+        T ds[6], pv[6], Pr[6][8];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) ds[a] = x[WideLayout::XDS + a];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) pv[a] = wv.lanev(pvi, 8 * a);
+        wv.sync();
+#pragma unroll
+        for (int a = 0; a < 6; ++a) ldn<8>(sp + 8 * a, Pr[a]);
+        T Lm[6][6], d[6];
+        bool ok = true;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            T s = (T)1 + ds[a] * ds[a] * Pr[a][a];
+#pragma unroll
+            for (int c = 0; c < a; ++c) s -= Lm[a][c] * Lm[a][c] * d[c];
+            d[a] = s;
+            ok = ok && (s > 0) && isfinite((double)s);
+#pragma unroll
+            for (int r = a + 1; r < 6; ++r) {
+                T q = ds[r] * ds[a] * Pr[r][a];
+#pragma unroll
+                for (int c = 0; c < a; ++c) q -= Lm[r][c] * Lm[a][c] * d[c];
+                Lm[r][a] = q / s;
+            }
+        }
+        bad = bad || !ok;
+        // right-hand sides: u = D^1/2 P[:, j], c = e_j / ds_j (j < 6), v = D^1/2 p -- then S^-1 of each
+        T u[6], c[6], v[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            T paj = Pr[a][0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q)
+                if (q == j) paj = Pr[a][q];
+            u[a] = ds[a] * paj;
+            c[a] = a == j ? (T)1 / ds[a] : (T)0;
+            v[a] = ds[a] * pv[a];
+        }
+        lsolve6(Lm, d, u);
+        lsolve6(Lm, d, c);
+        lsolve6(Lm, d, v);
+        // the lane's row i of the results (selects: no dynamic register indexing)
+        T ui = 0, ci = 0, vi = 0, dsi = 1;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            if (a == i) {
+                ui = u[a];
+                ci = c[a];
+                vi = v[a];
+                dsi = ds[a];
+            }
+        }
+        // P~ = M^T P = D^-1/2 S^-1 D^1/2 P and p~ = M^T p = D^-1/2 S^-1 D^1/2 p (no cancellation
+        // at either end of D); M = (I + D P)^-1 = D^1/2 S^-1 D^-1/2 for the step recursion
+        // and N = M - I = -D^1/2 S^-1 D^1/2 P, m = -D^1/2 S^-1 D^1/2 p for the rows' slack.
+        // (Rows / columns 6, 7 -- the previous control -- carry no soft row: M is the identity
+        // there, and the restoration problem's P has no entries in them.)
+        T Pt = Pij, pt = pvi;
+        if (i < 6) {
+            Pt = ui / dsi;
+            pt = vi / dsi;
+            if (j < 6) {
+                x[WideLayout::XM + 6 * i + j] = dsi * ci;
+                x[WideLayout::XMN + 6 * i + j] = -dsi * ui;
+            }
+            if (j == 0) x[WideLayout::XMV + i] = -dsi * vi;
+        }
+        wv.sync();  // every lane's reads of P are done
+        st(sp + t, Pt);
+        Pij = Pt;
+        pvi = pt;
+    }
+    // S^-1 b for S = L D L^T (6 x 6, unit lower L)
+    MPCG_HD static void lsolve6(const T (&Lm)[6][6], const T (&d)[6], T (&b)[6]) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+#pragma unroll
+            for (int c = 0; c < a; ++c) b[a] -= Lm[a][c] * b[c];
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) b[a] /= d[a];
+#pragma unroll
+        for (int a = 5; a >= 0; --a) {
+#pragma unroll
+            for (int r = a + 1; r < 6; ++r) b[a] -= Lm[r][a] * b[r];
+        }
+    }
+
+    // The step recursion through the soft rows (ds_k = M_k z_k + m_k, z_k the hard-dynamics
+    // image of stage k - 1, z_0 = -c_hat of the initial rows), the multipliers by the adjoint
+    // recursion (stationarity in s is unchanged), then the rows' steps
+    // dp = (dy - r_p)/(Sigma_p + dw), dn = -(dy + r_n)/(Sigma_n + dw) and the step statistics.
+    MPCG_HD Fwd forward_resto() {
+        const int t = wv.lane();
+        wv.sync();
+        T xs[NB][8], dus[NB][2], xlast[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lin[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int ks = t + 64 * b;
+            T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0, Mx[36], Nx[36], mv[6];
+            if (ks < N - 1) {
+                ldv<16>(L.KR(ks), K);
+                ldv<2>(L.KR(ks) + WideLayout::KF, kf);
+                ldv<8>(L.ST(ks) + WideLayout::SA, a);
+                ldv<6>(L.ST(ks) + WideLayout::SD, d);
+                if constexpr (MODEL == 1)
+                    ld2(L.ST(ks) + WideLayout::STW, twl, tvl);
+                else
+                    twl = dt;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) K[q] = 0;
+                kf[0] = 0;
+                kf[1] = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) a[q] = 0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) d[q] = 0;
+            }
+            if (ks < N) {
+                const T* x = xrec(ks);
+#pragma unroll
+                for (int q = 0; q < 36; ++q) {
+                    Mx[q] = x[WideLayout::XM + q];
+                    Nx[q] = x[WideLayout::XMN + q];
+                }
+#pragma unroll
+                for (int q = 0; q < 6; ++q) mv[q] = x[WideLayout::XMV + q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 36; ++q) {
+                    Mx[q] = 0;
+                    Nx[q] = 0;
+                }
+#pragma unroll
+                for (int q = 0; q < 6; ++q) mv[q] = 0;
+            }
+            T z[8];
+            if (b == 0) {
+                T c0[6];
+                ldv<6>(L.C0(), c0);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) z[j] = t == 0 ? c0[j] : (T)0;
+                z[6] = 0;
+                z[7] = 0;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) z[j] = t == 0 ? xlast[j] : (T)0;
+            }
+            const int steps = b == 0 ? (N < 64 ? N : 64) : N - 64;
+            T x[8], du0 = 0, du1 = 0, y[8], e[6];
+            for (int s = 0; s < steps; ++s) {
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    T ax = mv[r], ae = mv[r];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        ax += Mx[6 * r + c] * z[c];
+                        ae += Nx[6 * r + c] * z[c];
+                    }
+                    x[r] = ax;
+                    e[r] = ae;
+                }
+                x[6] = z[6];
+                x[7] = z[7];
+                T u0a = kf[0], u0b = 0, u1a = kf[1], u1b = 0;
+#pragma unroll
+                for (int m = 0; m < 8; m += 2) {
+                    u0a += K[m] * x[m];
+                    u0b += K[m + 1] * x[m + 1];
+                    u1a += K[8 + m] * x[m];
+                    u1b += K[9 + m] * x[m + 1];
+                }
+                du0 = u0a + u0b;
+                du1 = u1a + u1b;
+                A_mul(a, x, y);
+                if constexpr (MODEL == 1) {
+                    y[2] += tvl * x[3];
+                    y[5] += tvl * x[3];
+                }
+                y[2] += twl * du0;
+                y[3] += dt * du1;
+                y[5] += twl * du0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) y[j] += d[j];
+                y[6] = du0;
+                y[7] = du1;
+                wv.up8(z, y);
+            }
+            if (b == 0 && NB == 2) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xlast[j] = wv.lane63(y[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[b][j] = x[j];
+            dus[b][0] = du0;
+            dus[b][1] = du1;
+            // A ds + B du of the stage (the next rows' J dx = ds_{k+1} - this)
+            {
+                T l8[8];
+                A_mul(a, x, l8);
+                if constexpr (MODEL == 1) {
+                    l8[2] += tvl * x[3];
+                    l8[5] += tvl * x[3];
+                }
+                l8[2] += twl * du0;
+                l8[3] += dt * du1;
+                l8[5] += twl * du0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) lin[b][j] = ks < N - 1 ? l8[j] : (T)0;
+            }
+            if (ks < N) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) st(L.DW(ks) + j, x[j]);
+                st(L.DW(ks) + 6, du0);
+                st(L.DW(ks) + 7, du1);
+                T* xr = xrec(ks);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) xr[WideLayout::XE + j] = e[j];
+            }
+        }
+        wv.mark(3);
+        // the rows' multipliers: the adjoint recursion of stationarity in s (as forward_blk),
+        // lam_k = Q_k ds_k + q_k + A_k^T lam_{k+1}, y+ = -lam, except on the soft rows
+        // (D >= 0.6404 in Ipopt's scaled units, the Bunch-Kaufman 1x1 pivot test on the
+        // row's own diagonal) where y+ = D^-1 e (row form) -- the recursion loses digits
+        // there where a bound-active state's barrier Hessian is large, e / D does not;
+        // on nearly hard rows e / D would divide a slack's rounding by a small D
+        T lam_in[6] = {0, 0, 0, 0, 0, 0};
+        for (int b = NB - 1; b >= 0; --b) {
+            const int k = t + 64 * b;
+            T base[6] = {0, 0, 0, 0, 0, 0}, ak[8], tva = 0, yo[6] = {0, 0, 0, 0, 0, 0};
+            bool ov[6] = {false, false, false, false, false, false};
+            if (k < N) {
+                T qd[8], qv[8], cv[6], hvd = 0;
+                const int sb = L.ST(k);
+                ldv<8>(sb + WideLayout::SQD, qd);
+                ldv<8>(sb + WideLayout::SQV, qv);
+                ldv<6>(sb + WideLayout::SCV, cv);
+                ldv<8>(sb + WideLayout::SA, ak);
+                if constexpr (MODEL == 1) {
+                    tva = ld(sb + WideLayout::STV);
+                    hvd = ld(sb + WideLayout::SHVD);
+                }
+                const T* x = xs[b];
+                base[0] = (qd[0] + cv[0]) * x[0] + qv[0];
+                base[1] = qd[1] * x[1] + qv[1];
+                base[2] = (qd[2] + cv[1]) * x[2] + cv[2] * x[3] + qv[2];
+                base[3] = qd[3] * x[3] + cv[2] * x[2] + cv[4] * x[5] + qv[3];
+                base[4] = qd[4] * x[4] + qv[4];
+                base[5] = (qd[5] + cv[3]) * x[5] + cv[4] * x[3] + qv[5];
+                if constexpr (MODEL == 1) base[3] += hvd * dus[b][0];
+                const T* xr = xrec(k);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const T ds = xr[WideLayout::XDS + j], rsc = rowscale(j, k);
+                    const T dbar = ds * ds;
+                    ov[j] = dbar * rsc * rsc >= (T)0.6404;
+                    yo[j] = -xr[WideLayout::XE + j] / dbar;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ak[q] = 0;
+            }
+            T lam[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lam[q] = (b < NB - 1 && t == 63) ? lam_in[q] : (T)0;
+            const int steps = b == NB - 1 ? N - 64 * b : 64;
+            T o[6];
+            for (int s = steps - 1; s >= 0; --s) {
+                AT_mul(ak, lam, o);
+                if constexpr (MODEL == 1) o[3] += tva * (lam[2] + lam[5]);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) o[q] = ov[q] ? yo[q] : o[q] + base[q];
+                wv.dn6(lam, o);
+            }
+            if (k < N) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) st(L.YP(k) + q, -o[q]);
+            }
+            if (b > 0) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) lam_in[q] = wv.lane0(o[q]);
+            }
+        }
+        wv.mark(4);
+        wv.sync();
+        T linp[NB][6];
+        shift_blocks(lin, linp);
+        Fwd F{(T)1, (T)1, (T)0, (T)0};
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], gq[8], dk[8];
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<8>(L.ST(k) + WideLayout::SQV, gq);  // (the barrier gradient of x: precompute_resto)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) dk[q] = xs[b][q];
+            dk[6] = dus[b][0];
+            dk[7] = dus[b][1];
+            const int nv = last ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < nv) dir_var(w[j], zl[j], zu[j], vlo(j), vhi(j), gq[j], dk[j], F);
+            T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T irs = rcp(rowscale(j, k));
+                const T ys = ld(L.Y(k) + j) * irs, dys = (ld(L.YP(k) + j) - ld(L.Y(k) + j)) * irs;
+                const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+                const T zp = x[WideLayout::XZP + j], zn = x[WideLayout::XZN + j];
+                const T sp_ = zp / p + sv_delta, sn_ = zn / n + sv_delta;
+                const T gpp = (T)RHO - mu / p + (T)KD * mu, gpn = (T)RHO - mu / n + (T)KD * mu;
+                // the rows' steps: a variable whose Sigma dominates its unit coupling to the
+                // constraint row (the Bunch-Kaufman 1x1 pivot test, alpha = 0.6404) from its
+                // own row (dp = (y+ - gphi_p)/sp, dn = -(y+ + gphi_n)/sn), else from the
+                // constraint row dp - dn = J dx + c with J dx from the primal step -- never y+'s
+                // rounding divided by a small Sigma
+                const T ysn = ld(L.YP(k) + j) * irs;
+                const T q = rowscale(j, k) * (xs[b][j] - (k == 0 ? (T)0 : linp[b][j])) + x[WideLayout::XCR + j];
+                const T bk = (T)0.6404;
+                T dp, dn;
+                if (sp_ >= sn_) {
+                    dp = (ysn - gpp) / sp_;
+                    dn = sn_ >= bk ? -(ysn + gpn) / sn_ : dp - q;
+                } else {
+                    dn = -(ysn + gpn) / sn_;
+                    dp = sp_ >= bk ? (ysn - gpp) / sp_ : dn + q;
+                }
+                (void)ys;
+                x[WideLayout::XDP + j] = dp;
+                x[WideLayout::XDN + j] = dn;
+                dir_one(p, zp, gpp, dp, F);
+                dir_one(n, zn, gpn, dn, F);
+            }
+        }
+        T v[4] = {F.amax_p, F.amax_z, F.gd, F.rel};
+        const int op[4] = {RMIN, RMIN, RSUM, RMAX};
+        reduce<4, true>(v, op);
+        F.amax_p = v[0];
+        F.amax_z = v[1];
+        F.gd = v[2];
+        F.rel = v[3];
+        wv.mark(5);
+        return F;
+    }
+    // fraction to the boundary, grad phi^T d and the relative step of a variable with the
+    // lower bound 0 only
+    MPCG_HD void dir_one(T v, T z, T gphi, T dv, Fwd& F) const {
+        const T inf = (T)INFINITY;
+        F.amax_p = tmin(F.amax_p, dv < 0 ? -tau * v / dv : inf);
+        const T dz = mu / v - z - z / v * dv;
+        F.amax_z = tmin(F.amax_z, dz < 0 ? -tau * z / dz : inf);
+        F.gd += gphi * dv;
+        F.rel = tmax(F.rel, (T)fabs(dv) / ((T)1 + (T)fabs(v)));
+    }
+
+    // second-order correction right-hand side: c_soc = c_R(trial) + alpha c_soc (XCR)
+    MPCG_HD void soc_rhs_resto(T alpha) {
+        const int t = wv.lane();
+        wv.sync();
+        T w[NB][8], cs[NB][6];
+        load_w(w, alpha, true);
+        rows_c(w, cs);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T p = x[WideLayout::XP + j] + alpha * x[WideLayout::XDP + j];
+                const T n = x[WideLayout::XN + j] + alpha * x[WideLayout::XDN + j];
+                x[WideLayout::XCR + j] = (cs[b][j] - p + n) + alpha * x[WideLayout::XCR + j];
+            }
+        }
+        wv.sync();
+    }
+
+    // the restoration problem's primal-dual system error (soft restoration)
+    MPCG_HD T pd_error_resto() {
+        const int t = wv.lane();
+        wv.sync();
+        const T eta = eta_mu();
+        T w8[NB][8], cs[NB][6];
+        load_w(w8, (T)0, false);
+        rows_c(w8, cs);
+        T du = 0, pr_ = 0, cm = 0;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], y[6], yn[6] = {0, 0, 0, 0, 0, 0}, a[7] = {0, 0, 0, 0, 0, 0, 0};
+            T twk = dt, tvk = 0;
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<6>(L.Y(k), y);
+            if (!last) {
+                ldn<6>(L.Y(k + 1), yn);
+                Lin<T> ln;
+                ln.eval(pcoef().c, w);
+                ln.jac(w, dt, a);
+                turn_d(w, w + 6, &twk, &tvk);
+            }
+            T at[6] = {0, 0, 0, 0, 0, 0};
+            if (!last) {
+                AT_mul(a, yn, at);
+                if (model == 1) at[3] += tvk * (yn[2] + yn[5]);
+            }
+            const T btw = twk * (yn[2] + yn[5]), bta = dt * yn[3];
+            const int nv = last ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dr = dR(k, j);
+                    const T gq = eta * dr * dr * (w[j] - xR(k, j));
+                    const T gj = j < 6 ? gq + y[j] - at[j] : gq - (j == 6 ? btw : bta);
+                    du += fabs(gj - zl[j] + zu[j]);
+                    cm += fabs((w[j] - vlo(j)) * zl[j] - mu) + fabs((vhi(j) - w[j]) * zu[j] - mu);
+                }
+            }
+            const T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+                const T zp = x[WideLayout::XZP + j], zn = x[WideLayout::XZN + j];
+                const T ys = y[j] * rcp(rowscale(j, k));
+                pr_ += fabs(cs[b][j] - p + n);
+                du += fabs((T)RHO - ys - zp) + fabs((T)RHO + ys - zn);
+                cm += fabs(p * zp - mu) + fabs(n * zn - mu);
+            }
+        }
+        T v[3] = {du, pr_, cm};
+        const int op[3] = {RSUM, RSUM, RSUM};
+        reduce<3, true>(v, op);
+        const int nw = (8 * N - 2) + 12 * N, m = 6 * N, nbnd = 2 * (8 * N - 2) + 12 * N;
+        return wv.uni_d((v[0] + v[1] + v[2]) / (T)(nw + m + nbnd));
+    }
+
+    // copies of the lane-owned HBM records (RESTO; no-op otherwise): stage k's [xoff, xoff + n)
+    // to / from its spill copy at soff
+    MPCG_HD void xcopy(bool out, int xoff, int soff, int n) {
+        if constexpr (RESTO) {
+            const int t = wv.lane();
+            for (int b = 0; b < NB; ++b) {
+                const int k = t + 64 * b;
+                if (k >= N) continue;
+                T* x = xrec(k);
+                T* s = xsp + (size_t)k * WideLayout::XW + soff;
+                for (int q = 0; q < n; ++q) {
+                    if (out)
+                        s[q] = x[xoff + q];
+                    else
+                        x[xoff + q] = s[q];
+                }
+            }
+        }
     }
 
     // ------------------------------------------------------------ HBM spill area
@@ -2094,6 +3003,10 @@ struct WideSolver {
     // c_soc = c(w + alpha dw) + alpha c_soc on the dynamics rows (stage table SD) and the
     // initial-state rows (C0); the trial point is the last one tried (W + alpha DW).
     MPCG_HD void soc_rhs(T alpha) {
+        if constexpr (RESTO) {
+            soc_rhs_resto(alpha);
+            return;
+        }
         const int t = wv.lane();
         wv.sync();
         for (int b = 0; b < NB; ++b) {
@@ -2138,6 +3051,7 @@ struct WideSolver {
     // violation and the mu-complementarity, averaged over their 2(8N-2) + 6N + 8N-2
     // entries) of the iterate in LDS: the soft restoration phase's measure.
     MPCG_HD T pd_error() {
+        if constexpr (RESTO) return pd_error_resto();
         const int t = wv.lane();
         wv.sync();
         T du = 0, pr_ = 0, cm = 0;
@@ -2219,9 +3133,21 @@ struct WideSolver {
             st(L.ZL(k) + j, zln);
             st(L.ZU(k) + j, zun);
         }
+        if constexpr (RESTO) {
+            for (int b = 0; b < NB; ++b) {
+                const int k = t + 64 * b;
+                if (k >= N) continue;
+                T* x = xrec(k);
+#pragma unroll
+                for (int j = 0; j < 12; ++j) {  // (p, n then z_p, z_n: XZP = XP + 12)
+                    const T v = x[WideLayout::XP + j];
+                    x[WideLayout::XZP + j] = tmax(tmin(x[WideLayout::XZP + j], (T)1e10 * mu / v), mu / ((T)1e10 * v));
+                }
+            }
+        }
         wv.sync();
     }
-    // max |dy| of the direction (the tiny-step test's multiplier part)
+    // max |dy| of the direction (the tiny-step test's multiplier part; Ipopt's scaled multipliers)
     MPCG_HD T dy_max() {
         const int t = wv.lane();
         wv.sync();
@@ -2230,7 +3156,8 @@ struct WideSolver {
             const int k = t + 64 * b;
             if (k < N) {
 #pragma unroll
-                for (int j = 0; j < 6; ++j) m = tmax(m, (T)fabs(ld(L.YP(k) + j) - ld(L.Y(k) + j)));
+                for (int j = 0; j < 6; ++j)
+                    m = tmax(m, (T)fabs(ld(L.YP(k) + j) - ld(L.Y(k) + j)) * rcp(rowscale(j, k)));
             }
         }
         return rmax(m);
@@ -2247,7 +3174,7 @@ struct WideSolver {
     enum Op : int { OP_STATS = 0, OP_SOLVE = 1, OP_TRIAL = 2, OP_PDERR = 3, OP_SOCRHS = 4 };
     enum Ct : int {
         K_LSQ = 0, K_BEGIN, K_NEWTON, K_BT, K_SOCRHS, K_SOC, K_SOC_TRIAL, K_SOFT_TRIAL, K_SOFT_PD0, K_SOFT_PD1,
-        K_WD_STATS
+        K_WD_STATS, K_RMU
     };
     enum : int { LS_CONT = -1 };  // a continuation: the next sweep is set
     int op, ct;
@@ -2361,6 +3288,7 @@ struct WideSolver {
     // monotone barrier update (MonotoneMuUpdate::UpdateBarrierParameter) at the iterate
     // the statistics sweep just evaluated; then the Newton system.
     MPCG_HD int k_begin() {
+        if constexpr (RESTO) return k_begin_resto();
         acc_pending = false;
         const int nbnd = 2 * (8 * N - 2);
         const int ng = 6 * N;
@@ -2450,7 +3378,12 @@ struct WideSolver {
             else
                 delta_w = (dw_last == 0) ? (T)100 * delta_w : (T)8 * delta_w;
             ++inertia_attempt;
-            if (wv.uni((double)delta_w > 1e40 || !isfinite((double)delta_w))) return IPM_ERROR_IN_STEP;
+            // max_hessian_perturbation 1e20 (Ipopt 3.12's default): the iteration is skipped
+            // into the restoration phase; in the restoration problem it is an error
+            if (wv.uni((double)delta_w > 1e20 || !isfinite((double)delta_w))) {
+                if constexpr (RESTO) return IPM_ERROR_IN_STEP;
+                else return ls_goto_resto();
+            }
             return do_solve(0, delta_w, K_NEWTON);
         }
         if (sv_delta > 0) dw_last = sv_delta;
@@ -2465,11 +3398,11 @@ struct WideSolver {
             wd_short = 0;
             last_mu() = mu;
         }
-        if (P.acceptable_iter > 0 && cur_acceptable) {
+        if (!RESTO && P.acceptable_iter > 0 && cur_acceptable) {
             spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
             have_acc = 1;
         }
-        const T phik = wv.uni_d(sf * fval - mu * logsum);
+        const T phik = phi_cur();
         if (in_wd)
             set_ref(wd_theta(), wd_phi(), wd_gd());
         else
@@ -2539,6 +3472,7 @@ struct WideSolver {
             // Newton direction waits in the spill area
             spill_out(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
             spill_out(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+            xcopy(true, WideLayout::XDP, 36, 12);
             soc_count = 0;
             soc_alpha() = ls_alpha;
             soc_theta_old() = 0;
@@ -2557,6 +3491,7 @@ struct WideSolver {
         }
         spill_in(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
         spill_in(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
+        xcopy(false, WideLayout::XDP, 36, 12);
         ls_alpha *= (T)0.5;
         ++ls_n_steps;
         return bt_next();
@@ -2600,6 +3535,7 @@ struct WideSolver {
     MPCG_HD void start_watchdog(const Fwd& F) {
         in_wd = 1;
         spill_out(L.SP_WD(), 0, 52 * N);  // W, ZL, ZU, DW, Y, YP
+        xcopy(true, WideLayout::XP, 0, 36);  // (RESTO: p, n, z_p, z_n, dp, dn)
         wd_trial_iter = 0;
         wd_alpha_test() = F.amax_p;
         wd_amax_z() = F.amax_z;
@@ -2611,6 +3547,7 @@ struct WideSolver {
     MPCG_HD int stop_watchdog() {
         in_wd = 0;
         spill_in(L.SP_WD(), 0, 52 * N);
+        xcopy(false, WideLayout::XP, 0, 36);
         wd_short = 0;
         c_ok = 0;
         return do_stats(false, (T)0, (T)0, K_WD_STATS);
@@ -2645,31 +3582,19 @@ struct WideSolver {
         soft_ec() = pd_val;
         spill_out(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);  // W, ZL, ZU
         spill_out(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        xcopy(true, WideLayout::XP, 48, 24);  // (RESTO: p, n, z_p, z_n)
         accept_all(wv.lane(), true, soft_a(), soft_a(), false);
         c_ok = 0;
         return set_op(OP_PDERR, K_SOFT_PD1);
     }
     MPCG_HD int k_soft_pd1() {
         if (wv.uni(pd_val <= (T)P.soft_resto_factor * soft_ec())) {
-            // kappa_sigma correction of the accepted multipliers
-            const int t = wv.lane();
-            wv.sync();
-            const T bl[3] = {sl, wl, al}, bh[3] = {su, wu, au};
-            for (int e = t; e < 8 * N; e += 64) {
-                const int k = e >> 3, j = e & 7;
-                if (k == N - 1 && j >= 6) continue;
-                const T lo = j < 6 ? bl[0] : (j == 6 ? bl[1] : bl[2]);
-                const T hi = j < 6 ? bh[0] : (j == 6 ? bh[1] : bh[2]);
-                T zln, zun;
-                clamp_z(ld(L.W(k) + j), ld(L.ZL(k) + j), ld(L.ZU(k) + j), lo, hi, &zln, &zun);
-                st(L.ZL(k) + j, zln);
-                st(L.ZU(k) + j, zun);
-            }
-            wv.sync();
+            clamp_all();  // kappa_sigma correction of the accepted multipliers
             return soft_done(true, false);
         }
         spill_in(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);
         spill_in(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
+        xcopy(false, WideLayout::XP, 48, 24);
         return soft_done(false, false);
     }
     MPCG_HD int soft_done(bool accept, bool sat) {
@@ -2716,14 +3641,274 @@ struct WideSolver {
     }
     MPCG_HD int ls_fail() {
         if (!in_soft) augment_filter();
-        // almost feasible: the last acceptable iterate, if any, is the result
-        if (wv.uni(theta <= (T)1e-2 * (T)P.tol) && have_acc) {
-            spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
-            return IPM_ACCEPTABLE;
+        if constexpr (RESTO) {
+            return IPM_RESTORATION_FAILURE;  // (no restoration phase inside the restoration phase)
+        } else {
+            // almost feasible: the last acceptable iterate, if any, is the result
+            if (wv.uni(theta <= (T)1e-2 * (T)P.tol)) {
+                if (have_acc) {
+                    spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
+                    return IPM_ACCEPTABLE;
+                }
+                return IPM_RESTORATION_FAILURE;
+            }
+            in_soft = 0;
+            soft_count = 0;
+            wd_short = 0;
+            return NEED_RESTO;  // (solve() runs the restoration phase outside the state machine's loop)
         }
-        // Ipopt enters its feasibility restoration phase here (oracle/ipm.c
-        // perform_restoration); the device solver stops
-        return IPM_RESTORATION_FAILURE;
+    }
+    // FindAcceptableTrialPoint with the fallback to the restoration phase (the Newton
+    // system could not be made to have the right inertia)
+    MPCG_HD int ls_goto_resto() {
+        if (mu != last_mu()) {
+            in_wd = 0;
+            wd_short = 0;
+            last_mu() = mu;
+        }
+        if (P.acceptable_iter > 0 && cur_acceptable) {
+            spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
+            have_acc = 1;
+        }
+        if (in_wd) {  // the watchdog's stored iterate and direction, searched without skipping
+            wd_from_tiny = true;
+            return stop_watchdog();
+        }
+        return ls_fail();
+    }
+    // MinC_1NrmRestorationPhase::PerformRestoration: the original problem's LDS image goes to
+    // the workspace, the restoration problem runs out of line on the same LDS, and on success
+    // the image comes back with the new iterate (x of the restoration problem, y = 0, the
+    // bound multipliers of its step), which AcceptTrialPoint takes as the next iterate.
+    MPCG_HD int restoration() {
+        spill_out(L.SP_DUMP(), 0, L.total());
+        wv.gsync();
+        const RestoIn<T> in{mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, nf, iter};
+        const IpmParams Pc = P;
+        const RestoOut o = resto_phase<WV, MODEL, T, NB>(Pc, pr, wv, spill, in);
+        wv.gsync();
+        spill_in(L.SP_DUMP(), 0, L.total());
+        iter = wv.uni(o.iter);
+        c_ok = 0;
+        const int s = wv.uni(o.status);
+        if (s) return s;
+        clamp_all();
+        acc_pending = false;
+        ++iter;
+        return do_stats(false, (T)0, (T)0, K_BEGIN);
+    }
+
+    // ------------------------------------------------------------ the restoration phase's control
+    // (RESTO instance: oracle/ipm.c perform_restoration, resto_convergence and the
+    // restoration problem's pass through ipm_iterate / find_trial_point.)
+    MPCG_HD RestoOut run_resto(const RestoIn<T>& in) {
+        dumpO = spill + L.SP_DUMP();
+        ext = spill + L.SP_EXT();
+        xsp = spill + L.SP_XSP();
+        bounds_only();
+        sf = wv.uni_d((T)1);  // (RestoIpoptNLP: no objective scaling)
+        o_mu = wv.uni_d(in.mu);
+        o_tau = wv.uni_d(in.tau);
+        o_theta = wv.uni_d(in.theta);
+        o_ref_phi = wv.uni_d(in.ref_phi);
+        o_ref_theta = wv.uni_d(in.ref_theta);
+        o_sf = wv.uni_d(in.sf);
+        o_nf = wv.uni(in.nf);
+        // mu_R = max(mu, ||c||_inf), tau from it
+        mu = wv.uni_d(tmax(in.mu, in.prim_inf));
+        tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
+        status = 0;
+        theta_max() = -1;
+        theta_min = -1;
+        dw_last = 0;
+        delta_w_used = 0;
+        acc_alpha = 0;
+        acc_z = 0;
+        acc_pending = false;
+        iter = wv.uni(in.iter);
+        nf = 0;
+        kkt() = 0;
+        ref_theta = ref_phi = ref_gd = ref_pgd = ref_pth = 0;
+        last_rej_filter = count_filter_rej = n_filter_resets = 0;
+        in_wd = wd_short = wd_trial_iter = tiny_last = tiny_flag = in_soft = soft_count = acc_counter = have_acc = 0;
+        wd_alpha_test() = wd_theta() = wd_phi() = wd_gd() = wd_amax_z() = 0;
+        last_mu() = -1;
+        last_obj() = 0;
+        curr_obj() = (T)-1e50;
+        cur_acceptable = false;
+        st_acc = sv_ok = tr_ok = false;
+        st_alpha = st_z = tr_alpha = tr_test = tr_phi = tr_theta = pd_val = 0;
+        tr_acc = false;
+        ls_alpha = ls_alpha_max = ls_alpha_min = ls_alpha_test = ls_amax_z = 0;
+        ls_n_steps = inertia_attempt = soft_ctx = 0;
+        ls_eval_error = ls_skip_first = wd_from_tiny = false;
+        soc_alpha() = soc_amax_z() = soc_theta_old() = soc_theta_trial() = soft_ec() = soft_a() = 0;
+        soc_count = 0;
+        lsF = Fwd{(T)1, (T)1, (T)0, (T)0};
+        sv_F = lsF;
+        resto_first = true;
+        mu_Emu = 0;
+        mu_tf = 0;
+        mu_done = false;
+        init_rows();
+        do_stats(false, (T)0, (T)0, K_BEGIN);
+        run();
+        if (status == RESTO_DONE) {
+            resto_finish();
+            return RestoOut{0, iter};
+        }
+        return RestoOut{status, iter};
+    }
+
+    // RestoConvergenceCheck / RestoFilterConvergenceCheck::TestOrigProgress (from the second
+    // iterate on), then the restoration problem's own termination; then the monotone update.
+    MPCG_HD int k_begin_resto() {
+        acc_pending = false;
+        const int nbnd = 2 * (8 * N - 2) + 12 * N, ng = 6 * N;
+        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) * (T)0.01;
+        const T scc = tmax((T)100, l1z / (T)nbnd) * (T)0.01;
+        const T E0 = tmax(dual_inf / sd, tmax(prim_inf, compl0 / scc));
+#ifdef MPCG_TRACE
+        if (wv.lane() == 0)
+            printf("r%3d mu %.3e E0 %.3e dual %.3e prim %.3e compl %.3e th %.3e f %.10e thO %.3e phiO %.10e\n", iter,
+                   (double)mu, (double)E0, (double)dual_inf, (double)prim_inf, (double)compl0, (double)theta,
+                   (double)fval, (double)r_thO, (double)r_phiO);
+#endif
+        int s = 0;
+        if (!isfinite((double)E0) || !isfinite((double)theta) || !isfinite((double)fval)) {
+            s = IPM_INVALID_NUMBER;
+        } else {
+            if (resto_first)
+                resto_first = false;
+            else if (orig_progress())
+                s = RESTO_DONE;
+            if (!s) {
+                if (E0 <= (T)P.tol && dual_inf <= (T)P.dual_inf_tol && prim_inf <= (T)P.constr_viol_tol &&
+                    compl0 <= (T)P.compl_inf_tol)
+                    s = r_pinfO <= (T)1e2 * (T)P.tol ? IPM_FEASIBLE_POINT : IPM_LOCAL_INFEASIBILITY;
+                else if (iter >= P.max_iter)
+                    s = IPM_MAXITER;
+                else if (P.cpu_iter_budget >= 0 && iter > P.cpu_iter_budget)
+                    s = IPM_UNKNOWN;
+            }
+        }
+        s = wv.uni(s);
+        if (s) return s;
+        mu_tf = tiny_flag;
+        tiny_flag = 0;
+        mu_done = false;
+        mu_Emu = wv.uni_d(tmax(dual_inf / sd, tmax(prim_inf, tmax(pmax - mu, mu - pmin) / scc)));
+        return mu_loop();
+    }
+    // the barrier update's loop: each change of mu re-evaluates the restoration problem (its
+    // objective depends on mu), continued in k_rmu
+    MPCG_HD int mu_loop() {
+        const T kappa_eps = 10, kappa_mu = (T)0.2, theta_mu = (T)1.5;
+        const T mu_min = (T)(fmin(P.tol, P.compl_inf_tol) / 11.0);
+        for (;;) {
+            if (!wv.uni((mu_Emu <= kappa_eps * mu || mu_tf) && !mu_done)) break;
+            const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
+            const bool changed = mnew != mu;
+            if (!changed && mu_tf) return IPM_TINY_STEP;
+            mu = mnew;
+            tau = wv.uni_d(tmax((T)0.99, (T)1 - mu));
+            if (changed) return do_stats(false, (T)0, (T)0, K_RMU);
+            mu_done = true;
+            mu_tf = 0;
+        }
+        inertia_attempt = 0;
+        return do_solve(0, (T)0, K_NEWTON);
+    }
+    MPCG_HD int k_rmu() {
+        const int nbnd = 2 * (8 * N - 2) + 12 * N, ng = 6 * N;
+        const T sd = tmax((T)100, (l1y + l1z) / (T)(ng + nbnd)) * (T)0.01;
+        const T scc = tmax((T)100, l1z / (T)nbnd) * (T)0.01;
+        mu_Emu = wv.uni_d(tmax(dual_inf / sd, tmax(prim_inf, tmax(pmax - mu, mu - pmin) / scc)));
+        mu_done = wv.uni(mu_Emu > (T)10 * mu);
+        if (mu_done) {  // BacktrackingLineSearch::Reset
+            in_soft = 0;
+            in_wd = 0;
+            wd_short = 0;
+            nf = 0;
+        }
+        mu_tf = 0;
+        return mu_loop();
+    }
+    // the original problem accepts the restoration iterate x: its violation reduced below
+    // 0.9 of the value at the restoration start, acceptable to its filter and to its last
+    // reference point (from the restoration phase: no obj_max_inc test)
+    MPCG_HD bool orig_progress() {
+        if (!isfinite((double)r_phiO) || !isfinite((double)r_thO)) return false;
+        if (!wv.uni(r_thO <= (T)0.9 * o_theta)) return false;
+        const int t = wv.lane();
+        const int fi = L.FI();
+        bool hit = false;
+        for (int f0 = 0; f0 < o_nf; f0 += 64) {
+            const int f = f0 + t;
+            const bool h = f < o_nf && r_thO >= dumpO[fi + 2 * f] && r_phiO >= dumpO[fi + 2 * f + 1];
+            hit = hit || wv.any(h);
+        }
+        if (hit) return false;
+        const T gamma_theta = (T)1e-5, gamma_phi = (T)1e-8;
+        return wv.uni(compare_le(r_thO, ((T)1 - gamma_theta) * o_ref_theta, o_ref_theta) ||
+                      compare_le(r_phiO - o_ref_phi, -gamma_phi * o_ref_theta, o_ref_phi));
+    }
+    // back to the original problem: x from the restoration phase, y = 0 (constr_mult_reset_
+    // threshold 0), the bound multipliers by a Newton step of the complementarity with the
+    // whole restoration step as the primal step, cut by the fraction to the boundary
+    // (ComputeBoundMultiplierStep), all reset to 1 if one exceeds bound_mult_reset_threshold
+    // 1000 -- written into the original problem's LDS image
+    MPCG_HD void resto_finish() {
+        const int t = wv.lane();
+        wv.sync();
+        T* dmp = spill + L.SP_DUMP();
+        T amin = 1;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+            for (int j = 0; j < nv; ++j) {
+                const T x = ld(L.W(k) + j), w0 = dmp[L.W(k) + j];
+                const T zl = dmp[L.ZL(k) + j], zu = dmp[L.ZU(k) + j];
+                const T sc = w0 - vlo(j), sx = x - vlo(j), su = vhi(j) - w0, sxu = vhi(j) - x;
+                const T dl = (o_mu + zl * (sc - sx)) / sc - zl, du = (o_mu + zu * (su - sxu)) / su - zu;
+                if (dl < 0) amin = tmin(amin, -o_tau * zl / dl);
+                if (du < 0) amin = tmin(amin, -o_tau * zu / du);
+            }
+        }
+        const int opm[1] = {RMIN};
+        reduce<1, true>(&amin, opm);
+        T zmax = 0;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+            for (int j = 0; j < nv; ++j) {
+                const T x = ld(L.W(k) + j), w0 = dmp[L.W(k) + j];
+                const T zl = dmp[L.ZL(k) + j], zu = dmp[L.ZU(k) + j];
+                const T sc = w0 - vlo(j), sx = x - vlo(j), su = vhi(j) - w0, sxu = vhi(j) - x;
+                const T dl = (o_mu + zl * (sc - sx)) / sc - zl, du = (o_mu + zu * (su - sxu)) / su - zu;
+                zmax = tmax(zmax, tmax((T)fabs(zl + amin * dl), (T)fabs(zu + amin * du)));
+            }
+        }
+        const int opx[1] = {RMAX};
+        reduce<1, true>(&zmax, opx);
+        const bool reset = wv.uni(zmax > (T)1000);
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const int nv = k == N - 1 ? 6 : 8;
+            for (int j = 0; j < nv; ++j) {
+                const T x = ld(L.W(k) + j), w0 = dmp[L.W(k) + j];
+                const T zl = dmp[L.ZL(k) + j], zu = dmp[L.ZU(k) + j];
+                const T sc = w0 - vlo(j), sx = x - vlo(j), su = vhi(j) - w0, sxu = vhi(j) - x;
+                const T dl = (o_mu + zl * (sc - sx)) / sc - zl, du = (o_mu + zu * (su - sxu)) / su - zu;
+                dmp[L.ZL(k) + j] = reset ? (T)1 : zl + amin * dl;
+                dmp[L.ZU(k) + j] = reset ? (T)1 : zu + amin * du;
+                dmp[L.W(k) + j] = x;
+            }
+            for (int j = 0; j < 6; ++j) dmp[L.Y(k) + j] = 0;
+        }
     }
 
     MPCG_HD int step(int c) {
@@ -2738,12 +3923,93 @@ struct WideSolver {
             case K_SOFT_TRIAL: return k_soft_trial();
             case K_SOFT_PD0: return k_soft_pd0();
             case K_SOFT_PD1: return k_soft_pd1();
+            case K_RMU: return k_rmu();
             default: return k_wd_stats();
         }
     }
 
+    // The solve up to its end or to the start of a restoration phase (status NEED_RESTO):
+    // the kernel that runs the batch contains no call (a call site in the solver's loop costs
+    // the whole loop its register allocation); a problem that needs the restoration phase is
+    // parked (park()) and continued by a second kernel (unpark(), finish_resto()).
     MPCG_HD void solve() {
         init();
+        run();
+    }
+    // restoration phases and the solve after them, until the solve ends
+    MPCG_HD void finish_resto() {
+        if constexpr (!RESTO) {
+            while (status == NEED_RESTO) {
+                const int s = restoration();
+                if (s > 0) {
+                    status = s;
+                    break;
+                }
+                status = 0;
+                run();
+            }
+        }
+    }
+    // A parked problem: the solver's persistent scalars (PARK_SCALARS), its LDS image
+    // (WideLayout::total()), then a restoration workspace (WideLayout::slot(): the batch
+    // kernel's rare-path copies -- of which the acceptable point is kept -- and the restoration
+    // phase's records).
+    static constexpr int PARK_SCALARS = 32;
+    MPCG_HD static int park_elems(const WideLayout& L) { return PARK_SCALARS + L.total() + L.slot(); }
+    MPCG_HD void park(T* dst) {
+        const int t = wv.lane();
+        wv.sync();
+        if (t == 0) {
+            const T v[24] = {mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, theta_min, dw_last, delta_w_used,
+                             (T)iter, (T)nf, (T)last_rej_filter, (T)count_filter_rej, (T)n_filter_resets,
+                             (T)tiny_last, (T)tiny_flag, (T)acc_counter, (T)have_acc, (T)in_wd, (T)wd_short,
+                             (T)in_soft, (T)soft_count, (T)wd_trial_iter};
+            for (int i = 0; i < 24; ++i) dst[i] = v[i];
+        }
+        T* img = dst + PARK_SCALARS;
+        for (int e = t; e < L.total(); e += 64) img[e] = ld(e);
+        T* acc = img + L.total() + L.SP_ACC();
+        for (int e = t; e < WideLayout::WS * N; e += 64) acc[e] = spill[L.SP_ACC() + e];
+    }
+    // (the solver constructed with spill = park_entry + PARK_SCALARS + total())
+    MPCG_HD void unpark(const T* src) {
+        const int t = wv.lane();
+        setup();
+        wv.sync();
+        const T* img = src + PARK_SCALARS;
+        for (int e = t; e < L.total(); e += 64) st(e, img[e]);
+        wv.sync();
+        mu = wv.uni_d(src[0]);
+        tau = wv.uni_d(src[1]);
+        theta = wv.uni_d(src[2]);
+        prim_inf = wv.uni_d(src[3]);
+        ref_phi = wv.uni_d(src[4]);
+        ref_theta = wv.uni_d(src[5]);
+        sf = wv.uni_d(src[6]);
+        theta_min = wv.uni_d(src[7]);
+        dw_last = wv.uni_d(src[8]);
+        delta_w_used = wv.uni_d(src[9]);
+        iter = wv.uni((int)src[10]);
+        nf = wv.uni((int)src[11]);
+        last_rej_filter = wv.uni((int)src[12]);
+        count_filter_rej = wv.uni((int)src[13]);
+        n_filter_resets = wv.uni((int)src[14]);
+        tiny_last = wv.uni((int)src[15]);
+        tiny_flag = wv.uni((int)src[16]);
+        acc_counter = wv.uni((int)src[17]);
+        have_acc = wv.uni((int)src[18]);
+        in_wd = wv.uni((int)src[19]);
+        wd_short = wv.uni((int)src[20]);
+        in_soft = wv.uni((int)src[21]);
+        soft_count = wv.uni((int)src[22]);
+        wd_trial_iter = wv.uni((int)src[23]);
+        status = NEED_RESTO;
+        c_ok = 0;
+        acc_pending = false;
+        cur_acceptable = false;
+    }
+    // the state machine from the sweep set by init() / init_resto() to a status
+    MPCG_HD void run() {
         for (;;) {
             const int o = wv.uni(op);
             if (o == OP_STATS) {
@@ -2796,6 +4062,12 @@ struct WideSolver {
         return rsum(f);
     }
 };
+
+template <class WV, int MODEL, class T, int NB>
+MPCG_NOINLINE RestoOut resto_phase(const IpmParams& P, IpmProblem<T> pr, WV wv, T* ws, RestoIn<T> in) {
+    WideSolver<WV, MODEL, false, T, NB, true> R(P, pr, wv, ws);
+    return R.run_resto(in);
+}
 
 }  // namespace mpcg
 #endif

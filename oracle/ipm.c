@@ -25,7 +25,9 @@
  *   watchdog_trial_iter_max 3, soft_resto_pderror_reduction_factor 0.9999,
  *   max_soft_resto_iters 10, max_filter_resets 5, filter_reset_trigger 5,
  *   tiny_step_tol 10 eps, tiny_step_y_tol 1e-2,
- *   inertia correction delta_w0 1e-4, delta_w_min 1e-20, delta_w_max 1e40,
+ *   inertia correction delta_w0 1e-4, delta_w_min 1e-20, max_hessian_perturbation 1e20 (the
+ *   3.12 option default, IpPDPerturbationHandler.cpp; the paper's delta_w^max is 1e40) -- a
+ *   larger perturbation skips the iteration into the restoration phase,
  *   kappa_w- 1/3, kappa_w+ 8, kappa_w+bar 100, delta_c 1e-8 mu^0.25,
  *   bound_relax_factor 1e-8 (capped by constr_viol_tol 1e-4), honor_original_bounds,
  *   gradient-based NLP scaling (nlp_scaling_max_gradient 100),
@@ -567,7 +569,7 @@ static int factor_kkt(ipm* S) {
             else
                 delta_w = (S->dw_last == 0.0) ? 100.0 * delta_w : 8.0 * delta_w;
             ++attempt;
-            if (delta_w > 1e40) return 0;
+            if (delta_w > 1e20) return 0;
             continue;
         }
         for (int j = 0; j < nw; ++j)
@@ -594,7 +596,7 @@ static int factor_kkt(ipm* S) {
         else
             delta_w = (S->dw_last == 0.0) ? 100.0 * delta_w : 8.0 * delta_w;
         ++attempt;
-        if (delta_w > 1e40) return 0;
+        if (delta_w > 1e20) return 0;
     }
 }
 /* Solve the factored system for the step with constraint right-hand side -crhs; the

@@ -16,6 +16,7 @@
 //         B, then B x (state[6], coeffs[4])
 // stdout: per problem: status iters obj u0[2] traj[3N]
 #include <barrier>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <thread>
@@ -43,6 +44,7 @@ struct HostWave {
     template <class U>
     U* Sp() const { return reinterpret_cast<U*>(lds); }
     void sync() const { sh->bar.arrive_and_wait(); }
+    void gsync() const { sync(); }
     template <class U>
     U from(U v, int src) const {
         sh->xd[t] = (double)v;
@@ -127,6 +129,8 @@ struct HostWave {
     U lane63(U v) const { return from(v, 63); }
     template <class U>
     U lane0(U v) const { return from(v, 0); }
+    template <class U>
+    U lanev(U v, int l) const { return from(v, l); }
     // reduction partners of the device (wave_dev.h): xor 1, xor 2, mirror 8, mirror 16, xor 16, xor 32
     template <int s, class U>
     U rpart(U v) const {
@@ -165,7 +169,8 @@ int main() {
         for (HT& v : pr.c) { double d; std::scanf("%lf", &d); v = (HT)d; }
         HostShared sh;
         sh.lds.assign(L.total(), std::nan(""));
-        std::vector<HT> spill(L.spill(), (HT)std::nan(""));
+        std::vector<HT> spill(L.slot(), (HT)std::nan(""));
+        std::vector<HT> park(32 + L.total() + L.slot(), (HT)std::nan(""));
         int status = 0, iters = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
@@ -173,8 +178,19 @@ int main() {
         for (int t = 0; t < 64; ++t) {
             th.emplace_back([&, t]() {
                 HostWave wv{&sh, t, sh.lds.data()};
-                auto run = [&](auto& S) {
-                    S.solve();
+                auto run = [&](auto& S0) {
+                    typedef std::decay_t<decltype(S0)> Solver;
+                    S0.solve();
+                    // a restoration phase: parked and continued as the device's second kernel does
+                    Solver S2(P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
+                    const bool parked = S0.status == Solver::NEED_RESTO;
+                    if (parked) {
+                        S0.park(park.data());
+                        sh.bar.arrive_and_wait();
+                        S2.unpark(park.data());
+                        S2.finish_resto();
+                    }
+                    Solver& S = parked ? S2 : S0;
                     const double o = S.objective_out();
                     if (t == 0) {
                         status = S.status;

@@ -89,15 +89,21 @@ def test_param_defaults_and_keys(libmpcg):
 
 
 def test_workspace_bytes(libmpcg):
-    """Spill areas (114 N doubles per problem) plus the solve-order buffers beyond 2048."""
+    """One workspace slot per resident wavefront (not per problem) and a park area for the
+    problems that enter the restoration phase, plus the solve-order buffers beyond 2048.
+    N = 20: a slot is 114N = 2280 doubles (rare-path copies), a park entry 32 + 2492 (LDS
+    image) + 8852 (the rare-path copies, 2492 for the original problem's image and 204N of
+    restoration records); without a GPU the slot count falls back to 4096."""
     from mpc_ros_amd import _lib
 
     p = _lib.MpcgParams()
     libmpcg.mpcg_params_plugin_default(C.byref(p))
     b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
-    assert b1 == 114 * 20 * 8
-    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 2048) == 2048 * b1
-    assert libmpcg.mpcg_workspace_bytes(C.byref(p), 65536) > 65536 * b1
+    assert b1 == 3 * 256 + (2280 + 11376) * 8
+    b2 = libmpcg.mpcg_workspace_bytes(C.byref(p), 2)
+    assert b2 == 3 * 256 + 2 * (2280 + 11376) * 8
+    big = libmpcg.mpcg_workspace_bytes(C.byref(p), 65536)
+    assert big < 65536 * 2280 * 8 // 4  # (bounded by residency, not by B)
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
 
 

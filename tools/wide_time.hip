@@ -8,6 +8,7 @@
 // reports the largest u0 difference to that file (another variant's output).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I <csrc dir> tools/wide_time.hip -o wt
+// (-DWT_OLD_API for sources from before round 3's workspace-size argument)
 //   ./wt inputs.bin out_u0.bin [ref_u0.bin]
 #include <hip/hip_runtime.h>
 
@@ -73,7 +74,12 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(e0));
         int32_t* order = nullptr;
         CK(mpcg::launch_wide_order(B, dcf, dsched, sb, &order, 0));
+#ifdef WT_OLD_API
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill, 0));
+#else
+        CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill,
+                                   mpcg::wide_spill_bytes(P, B), 0));
+#endif
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms = 0;
