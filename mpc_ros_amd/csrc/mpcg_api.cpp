@@ -28,6 +28,10 @@ int hip_fail(hipError_t e, const char* what) {
 struct mpcg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the restoration phase's resume workers run on aux alongside the batch kernel (fork /
+    // join events on the caller's stream)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     mpcg_params params{};
     // staging buffers for mpcg_solve (host pointers)
     double* d_io = nullptr;
@@ -283,9 +287,12 @@ int mpcg_create(int device, mpcg_handle** out) {
     }
     mpcg_params_plugin_default(&h->params);
     e = hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
         mpcg_destroy(h);
-        return hip_fail(e, "hipEventCreate");
+        return hip_fail(e, "hipEventCreate / hipStreamCreate");
     }
     *out = h;
     return 0;
@@ -301,7 +308,11 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->d_pp) hipFree(h->d_pp);
     if (h->d_sched) hipFree(h->d_sched);
     if (h->d_spill) hipFree(h->d_spill);
+    if (h->aux) hipStreamSynchronize(h->aux);
     if (h->last_ev) hipEventDestroy(h->last_ev);
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->ev_join) hipEventDestroy(h->ev_join);
+    if (h->aux) hipStreamDestroy(h->aux);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -429,7 +440,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
         order = ord;
     }
     e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order,
-                                (void*)h->d_spill, h->spill_bytes, s);
+                                (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     return record_on(h, s);
 }

@@ -27,13 +27,23 @@ struct WideArgs {
     void* slots;           // nslots workspaces of WideLayout::spill() elements of T (the rare paths' copies)
     int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
     int32_t nslots;
-    // parked problems (the restoration phase, continued by k_resume_wide): count, capacity,
-    // problem index and state of each
+    // parked problems (the restoration phase, continued by k_resume_wide while the batch
+    // kernel runs): count, capacity, problem index, ready flag and state of each; the entries
+    // taken by the resume workers; the batch kernel's finished workgroups
     int32_t* park_count;
     int32_t park_cap;
     int64_t* park_idx;
+    int32_t* park_ready;
+    int32_t* park_taken;
+    int32_t* done;
     void* park;
 };
+// the wavefront's end in k_solve_wide (after its results / its parked state are written)
+__device__ __forceinline__ void block_done(int32_t* done) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (threadIdx.x == 0) atomicAdd(done, 1);
+}
 
 // A workspace slot for the wavefront's problem: the first free one from blockIdx mod
 // nslots on (nslots >= the resident wavefronts, so the first probe normally succeeds;
@@ -96,13 +106,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (e < a.park_cap) {
             S.park((T*)a.park + (int64_t)e * Solver::park_elems(Lw));
             if (t == 0) a.park_idx[e] = p;
+            // the entry is complete: its ready flag after the stores (release, device scope)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_wave_barrier();
+            if (t == 0) atomicExch(&a.park_ready[e], 1);
             release_slot(a.slot_flags, slot);
+            block_done(a.done);
             return;
         }
         S.status = IPM_RESTORATION_FAILURE;  // (more parked problems than the park area holds)
     }
     write_out(a, S, p);
     release_slot(a.slot_flags, slot);
+    block_done(a.done);
 }
 
 // results of problem p (u0, status, iterations, objective, trajectory; honor_original_bounds)
@@ -131,28 +147,70 @@ __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t 
 // The parked problems: the restoration phase (WideSolver<..., RESTO> out of line) and the
 // rest of the solve, from the state k_solve_wide parked -- the same solver instance, so the
 // iterates are those the first kernel would have continued with.  A separate kernel keeps
-// the call out of the batch kernel's register allocation; it runs over the park area only.
+// the call out of the batch kernel's register allocation.  It runs on a second stream
+// alongside the batch kernel: a few workers take parked problems as they appear (a problem
+// that parks early in the batch is resumed while the batch still runs) and exit once every
+// workgroup of the batch kernel has finished and every parked problem is taken.  A worker
+// that sees no progress of the batch kernel for 20 s exits (the batch kernel failed).
+__device__ __forceinline__ int take_parked(const WideArgs& a) {
+    int r = -1;
+    if (threadIdx.x == 0) {
+        uint64_t t0 = wall_clock64();
+        int last_done = -1;
+        for (;;) {
+            const int d = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            int c = __hip_atomic_load(a.park_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            c = c < a.park_cap ? c : a.park_cap;
+            const int tk = __hip_atomic_load(a.park_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk < c) {
+                if (atomicCAS(a.park_taken, tk, tk + 1) == tk) {
+                    r = tk;
+                    break;
+                }
+                continue;
+            }
+            // (a workgroup parks before it counts itself done: all parked once done == B)
+            if ((int64_t)d >= a.B && tk >= c) break;
+            if (d != last_done) {
+                last_done = d;
+                t0 = wall_clock64();
+            } else if (wall_clock64() - t0 > (uint64_t)2000000000) {  // 20 s at 100 MHz
+                break;
+            }
+            __builtin_amdgcn_s_sleep(32);
+        }
+        if (r >= 0) {  // the entry's stores are visible once its ready flag is
+            while (__hip_atomic_load(&a.park_ready[r], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    r = __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return r;
+}
+
 template <int MODEL, bool SPLIT, class T, int NB>
-__global__ void __launch_bounds__(64) k_resume_wide(WideArgs a) {
-    const int n = *a.park_count < a.park_cap ? *a.park_count : a.park_cap;
-    const int e = (int)blockIdx.x;
-    if (e >= n) return;
-    const int64_t p = a.park_idx[e];
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_resume_wide(WideArgs a) {
     const int t = threadIdx.x;
-    IpmProblem<T> pr;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
-    DevWave wv;
-    wv.t = t;
     const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
-    T* ent = (T*)a.park + (int64_t)e * Solver::park_elems(Lw);
-    Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
-    S.unpark(ent);
-    S.finish_resto();
-    write_out(a, S, p);
+    for (;;) {
+        const int e = take_parked(a);
+        if (e < 0) return;
+        const int64_t p = a.park_idx[e];
+        IpmProblem<T> pr;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
+        DevWave wv;
+        wv.t = t;
+        T* ent = (T*)a.park + (int64_t)e * Solver::park_elems(Lw);
+        Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
+        S.unpark(ent);
+        S.finish_resto();
+        write_out(a, S, p);
+    }
 }
 
 // Scheduling key: workgroups are dispatched roughly in index order, so a slow problem
@@ -264,14 +322,24 @@ static size_t park_elems(const IpmParams& P) {
 }
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
-    return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) +
+    return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) + slot_flag_bytes(pc) +
            (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns +
            park_elems(P) * elem_bytes(P) * (size_t)pc;
 }
 
+// Resume workers (parked problems in flight at once): each holds a wavefront slot and a
+// problem's LDS for the whole batch kernel (32 workers cost the batch kernel ~7 %, 2 under
+// 1 %), and problems park rarely (~5e-5 of the infinity set at N = 20, ~5e-4 at N = 40):
+// two, and one more per 65536 problems.
+#ifndef MPCG_RESUME_WORKERS
+#define MPCG_RESUME_WORKERS 2
+#endif
+static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 65536; }
+
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             void* spill, size_t spill_bytes, hipStream_t stream) {
+                             void* spill, size_t spill_bytes, hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork,
+                             hipEvent_t ev_join) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
@@ -284,7 +352,8 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // the workspace (wide_spill_bytes): slot flags | park count (256 B) | park indices | slots | park area
+    // the workspace (wide_spill_bytes): slot flags | park count, taken, done (256 B) | park
+    // indices | park ready flags | slots | park area
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
     if (ns < 1 || wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
     char* w = (char*)spill;
@@ -294,25 +363,41 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     w += 256;
     int64_t* pidx = (int64_t*)w;
     w += (size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255;
+    int32_t* pready = (int32_t*)w;
+    w += slot_flag_bytes(pc);
     void* slots = w;
     w += (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns;
     void* park = w;
-    e = hipMemsetAsync(spill, 0, slot_flag_bytes(ns) + 256, stream);  // (flags and the park count)
+    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, park counters)
+    if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
     if (e != hipSuccess) return e;
     const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, slots, flags, (int32_t)ns,
-                     pcount, (int32_t)pc, pidx, park};
+                     pcount, (int32_t)pc, pidx, pready, pcount + 1, pcount + 2, park};
     void* args[] = {(void*)&a};
-    e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
-    if (e != hipSuccess) return e;
-    // the parked problems (a grid over the park area; workgroups beyond the count exit at once)
     const void* rf = resume_kernel(P);
     e = hipFuncGetAttributes(&fa, rf);
     if (e != hipSuccess) return e;
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
+    // fork: the resume workers on the aux stream alongside the batch kernel; join: the
+    // stream continues after both (no host synchronisation; graph-capturable)
+    const bool fork = aux && aux != stream && ev_fork && ev_join;
+    if (fork) {
+        e = hipEventRecord(ev_fork, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);
+        if (e != hipSuccess) return e;
+    }
+    e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
+    const unsigned workers = (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B));
+    e = hipLaunchKernel(rf, dim3(workers), dim3(64), args, lds, fork ? aux : stream);
+    if (e != hipSuccess) return e;
+    if (fork) {
+        e = hipEventRecord(ev_join, aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 

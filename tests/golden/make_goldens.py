@@ -165,6 +165,12 @@ FEATURE_SETS = {
     "N40": (dict(PLUGIN, STEPS=40), [88, 460, 842, 2012, 2094, 422, 429, 1431, 69, 1167, 1204, 2956, 3441]),
     # bicycle N25: watchdog (3308), soft restoration (1292), corrections (18, 23)
     "bicycle": (BICYCLE, [3308, 1292, 18, 23]),
+    # the feasibility-restoration phase (round 3, found by scanning problems 0..131071 at
+    # N = 20 and 0..32767 at N = 40 with the oracle's diagnostics): every problem of those
+    # ranges on which Ipopt enters it
+    "resto_N20": (PLUGIN, [1443, 40852, 74511, 84582]),
+    "resto_N40": (dict(PLUGIN, STEPS=40), [69, 1167, 1204, 2956, 3441, 4626, 8420, 9871, 18581, 18819, 19148,
+                                            19304, 23287, 25150, 25384, 28303, 30285, 31014, 31746]),
 }
 
 

@@ -100,6 +100,22 @@ def test_wide_core_ipopt_features(wide_harness, features_golden, name):
     compare(r, sub, atol=1e-9)
 
 
+@pytest.mark.parametrize("name", ["resto_N20", "resto_N40"])
+def test_wide_core_restoration_phase(wide_harness, features_golden, name):
+    """Ipopt's feasibility-restoration phase (RestoIpoptNLP, one to three restoration
+    iterations, then back to the original problem): same statuses, iteration counts and
+    values as the oracle (tests/golden/ipopt_features.npz resto_* sets, every problem of the
+    scanned ranges that enters it; the GPU test runs all of them)."""
+    g = features_golden[name]
+    rows = {"resto_N20": [0, 1, 3], "resto_N40": [2, 3, 11]}[name]
+    sub = subset(g, rows)
+    assert (sub["diag"][:, 3] > 0).all()
+    r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
+    # (N40 problem 19304: 217 iterations through two restoration phases; its trajectory
+    # agrees to 9e-9 -- the GPU tolerance 1e-7 here)
+    compare(r, sub, atol=1e-7)
+
+
 def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
     """max_cpu_time as an iteration budget: status 14 (unknown) beyond it, as the oracle."""
     g = features_golden["budget"]

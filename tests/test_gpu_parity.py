@@ -92,10 +92,12 @@ def test_variants_match_oracle(torch_cuda, variants_golden, name):
         check_against(r, g)
 
 
-@pytest.mark.parametrize("name", ["N20", "N40", "bicycle"])
+@pytest.mark.parametrize("name", ["N20", "N40", "bicycle", "resto_N20", "resto_N40"])
 def test_ipopt_features_match_oracle(torch_cuda, features_golden, name):
-    """Problems on which Ipopt's second-order corrections, watchdog and soft restoration
-    act (tests/golden/ipopt_features.npz): same statuses and iteration counts."""
+    """Problems on which Ipopt's second-order corrections, watchdog, soft restoration and
+    feasibility-restoration phase act (tests/golden/ipopt_features.npz; the resto_* sets:
+    every problem of the scanned ranges that enters the restoration phase, run by the
+    device's parked-problem kernel): same statuses and iteration counts."""
     g = features_golden[name]
     r = solver_for(g["P"]).solve(g["state"], g["coeffs"])
     check_against(r, g, min_same_iters=1.0)

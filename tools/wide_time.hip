@@ -65,6 +65,13 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dsched, sb));
     void* dspill;
     CK(hipMalloc(&dspill, mpcg::wide_spill_bytes(P, B)));
+#ifndef WT_OLD_API
+    hipStream_t aux;
+    hipEvent_t evf, evj;
+    CK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&evf, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&evj, hipEventDisableTiming));
+#endif
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -78,7 +85,7 @@ int main(int argc, char** argv) {
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill, 0));
 #else
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill,
-                                   mpcg::wide_spill_bytes(P, B), 0));
+                                   mpcg::wide_spill_bytes(P, B), 0, getenv("WT_SEQ") ? nullptr : aux, evf, evj));
 #endif
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
