@@ -155,6 +155,17 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
 
+/* mpcg_solve / mpcg_solve_device with per-problem solver diagnostics diag [B][4] (int32,
+ * may be NULL): restoration phases entered, filter entries dropped beyond its capacity
+ * (filter_cap in LDS plus 448 in the workspace; Ipopt's filter is unbounded, so any nonzero
+ * value marks a solve that may differ from Ipopt's), 1 if the problem was continued by the
+ * parked-problem kernel, 0. */
+int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
+                  int32_t* status, double* obj, int32_t* iters, int32_t* diag);
+int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
+                         double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, int32_t* d_diag,
+                         void* stream);
+
 /* Multi-GPU batched solve from one process, host buffers as
  * mpcg_solve: the B problems are split into ngpu contiguous shards (the first B % ngpu
  * GPUs take one more), solved on devices[r] with the given parameters, and the results are

@@ -62,6 +62,9 @@ SIGNATURES = {
     "mpcg_solve": ([C.c_void_p, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip], C.c_int),
     "mpcg_solve_device": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    "mpcg_solve_ex": ([C.c_void_p, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip, _ip], C.c_int),
+    "mpcg_solve_device_ex": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_preprocess_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                 C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_track_device": ([C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,

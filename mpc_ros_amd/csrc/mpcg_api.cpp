@@ -411,6 +411,12 @@ int mpcg_get_strategy(const mpcg_handle* h) {
 
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream) {
+    return mpcg_solve_device_ex(h, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, nullptr, stream);
+}
+
+int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
+                         double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, int32_t* d_diag,
+                         void* stream) {
     if (!h) return fail(-1, "null handle");
     if (B < 0) return fail(-1, "negative batch");
     if (B == 0) return 0;
@@ -439,7 +445,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
         if (e != hipSuccess) return hip_fail(e, "solve-order sort");
         order = ord;
     }
-    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, order,
+    e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, d_diag, order,
                                 (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     return record_on(h, s);
@@ -447,6 +453,11 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
 
 int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
                int32_t* status, double* obj, int32_t* iters) {
+    return mpcg_solve_ex(h, B, state, coeffs, u0, traj, status, obj, iters, nullptr);
+}
+
+int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
+                  int32_t* status, double* obj, int32_t* iters, int32_t* diag) {
     if (!h) return fail(-1, "null handle");
     if (B < 0) return fail(-1, "negative batch");
     if (B == 0) return 0;
@@ -454,8 +465,9 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
     int rc = mpcg_params_check(&h->params);
     if (rc) return rc;
     const int N = h->params.steps;
-    // io block: state 6 | coeffs 4 | u0 2 | traj 3N | obj 1 | status+iters (2 int32 = 1 double)
-    const size_t per = (size_t)(6 + 4 + 2 + 3 * N + 1 + 1);
+    // io block: state 6 | coeffs 4 | u0 2 | traj 3N | obj 1 | status+iters (2 int32 = 1 double) |
+    // diag (4 int32 = 2 doubles)
+    const size_t per = (size_t)(6 + 4 + 2 + 3 * N + 1 + 1 + 2);
     const size_t need = per * sizeof(double) * (size_t)B;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
@@ -477,10 +489,11 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
     double* dob = dt + (size_t)3 * N * B;
     int32_t* dst = (int32_t*)(dob + B);
     int32_t* dit = dst + B;
+    int32_t* ddg = dit + B;
     e = hipMemcpyAsync(ds, state, sizeof(double) * 6 * B, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dc, coeffs, sizeof(double) * 4 * B, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy H2D");
-    rc = mpcg_solve_device(h, B, ds, dc, du, dt, dst, dob, dit, h->stream);
+    rc = mpcg_solve_device_ex(h, B, ds, dc, du, dt, dst, dob, dit, diag ? ddg : nullptr, h->stream);
     if (rc) return rc;
     e = hipMemcpyAsync(u0, du, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && traj)
@@ -490,6 +503,8 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
         e = hipMemcpyAsync(status, dst, sizeof(int32_t) * B, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && iters)
         e = hipMemcpyAsync(iters, dit, sizeof(int32_t) * B, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && diag)
+        e = hipMemcpyAsync(diag, ddg, sizeof(int32_t) * 4 * B, hipMemcpyDeviceToHost, h->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy D2H");
     e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");

@@ -17,8 +17,9 @@ size_t wide_lds_bytes(const IpmParams& P);
 size_t wide_spill_bytes(const IpmParams& P, int64_t B);
 int64_t wide_slots(const IpmParams& P, int64_t B);
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
-                             double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             void* spill, size_t spill_bytes, hipStream_t stream, hipStream_t aux = nullptr,
+                             double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
+                             const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
+                             hipStream_t aux = nullptr,
                              hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the
 // launch that writes the workgroup -> problem map into `buf` (returned in *order).

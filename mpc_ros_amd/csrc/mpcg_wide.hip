@@ -24,6 +24,7 @@ struct WideArgs {
     int32_t* status;
     double* obj;
     int32_t* iters;
+    int32_t* diag;         // [B][4] restoration phases, filter overflows, parked, 0 (or null)
     void* slots;           // nslots workspaces of WideLayout::spill() elements of T (the rare paths' copies)
     int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
     int32_t nslots;
@@ -77,7 +78,7 @@ __device__ __forceinline__ void release_slot(int32_t* flags, int s) {
 // DEFOPT: the Ipopt options are the reference's defaults (ipopt_default_options), compiled
 // as constants.
 template <class Solver>
-__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p);
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked);
 
 template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
@@ -116,15 +117,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         }
         S.status = IPM_RESTORATION_FAILURE;  // (more parked problems than the park area holds)
     }
-    write_out(a, S, p);
+    write_out(a, S, p, 0);
     release_slot(a.slot_flags, slot);
     block_done(a.done);
 }
 
 // results of problem p (u0, status, iterations, objective, trajectory; honor_original_bounds)
 template <class Solver>
-__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p) {
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked) {
     const int t = threadIdx.x;
+    if (a.diag && t == 0) {
+        a.diag[p * 4 + 0] = S.n_resto;
+        a.diag[p * 4 + 1] = S.n_fover;
+        a.diag[p * 4 + 2] = parked;
+        a.diag[p * 4 + 3] = S.nf_peak;
+    }
     const double o = (double)S.objective_out();
     const int N = a.P.N;
     if (t == 0) {
@@ -209,7 +216,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
         S.unpark(ent);
         S.finish_resto();
-        write_out(a, S, p);
+        write_out(a, S, p, 1);
     }
 }
 
@@ -337,9 +344,9 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
 static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 65536; }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
-                             double* traj, int32_t* status, double* obj, int32_t* iters, const int32_t* order,
-                             void* spill, size_t spill_bytes, hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork,
-                             hipEvent_t ev_join) {
+                             double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
+                             const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
+                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
@@ -371,7 +378,7 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, park counters)
     if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
     if (e != hipSuccess) return e;
-    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, slots, flags, (int32_t)ns,
+    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, diag, slots, flags, (int32_t)ns,
                      pcount, (int32_t)pc, pidx, pready, pcount + 1, pcount + 2, park};
     void* args[] = {(void*)&a};
     const void* rf = resume_kernel(P);

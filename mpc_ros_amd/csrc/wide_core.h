@@ -94,7 +94,12 @@ struct WideLayout {
     MPCG_HD int SP_ACC() const { return 52 * N; }
     MPCG_HD int SP_SOC() const { return 62 * N; }
     MPCG_HD int SP_SOFT() const { return 78 * N; }
-    MPCG_HD int spill() const { return 114 * N; }
+    // The filter beyond its cap LDS entries: FX more in the workspace (Ipopt's filter is
+    // unbounded; the infinity set reaches 71 entries at N = 40), the original problem's at
+    // SP_FLT, the restoration problem's at SP_FLTR
+    static constexpr int FX = 448;
+    MPCG_HD int SP_FLT() const { return 114 * N; }
+    MPCG_HD int spill() const { return 114 * N + 2 * FX; }
     // The feasibility-restoration phase (WideSolver<..., RESTO = true>, entered from the
     // original problem's line search): the original problem's LDS image while the
     // restoration problem uses the LDS (total()), the restoration problem's per-stage
@@ -114,7 +119,8 @@ struct WideLayout {
     MPCG_HD int SP_DUMP() const { return spill(); }
     MPCG_HD int SP_EXT() const { return spill() + total(); }
     MPCG_HD int SP_XSP() const { return SP_EXT() + XS * N; }
-    MPCG_HD int slot() const { return SP_XSP() + XW * N; }
+    MPCG_HD int SP_FLTR() const { return SP_XSP() + XW * N; }
+    MPCG_HD int slot() const { return SP_FLTR() + 2 * FX; }
 };
 
 // The original problem's values the restoration phase needs (passed by value into its
@@ -127,6 +133,7 @@ struct RestoIn {
 struct RestoOut {
     int status;  // 0: the restoration phase found a point the original problem accepts
     int iter;
+    int fover;  // its filter's dropped entries (diagnostic)
 };
 // The restoration phase of the problem whose wavefront state is in LDS and whose workspace
 // slot is ws (defined after WideSolver; out of line).
@@ -185,6 +192,9 @@ struct WideSolver {
     int in_wd, wd_short, wd_trial_iter, tiny_last, tiny_flag, in_soft, soft_count, acc_counter, have_acc;
 
     T* spill;  // this problem's HBM spill area (WideLayout::spill() elements)
+    int n_fover = 0;  // filter entries dropped beyond cap + FX (diagnostic; Ipopt drops none)
+    int nf_peak = 0;  // the most filter entries held at once (diagnostic)
+    int n_resto = 0;  // restoration phases entered (diagnostic)
     // Rarely used wave-uniform solver state lives in the problem's LDS control block
     // (registers are the scarcer resource: every scalar held across the iteration loop
     // competes with the sweeps).  x() = v stores (lane 0), x() reads (uniform).
@@ -2889,63 +2899,86 @@ struct WideSolver {
         return compare_le(thetat, ((T)1 - gamma_theta) * ref_theta, ref_theta) ||
                compare_le(phit - ref_phi, -gamma_phi * ref_theta, ref_phi);
     }
+    // filter entry f (theta, phi): the first filter_cap in LDS, the next WideLayout::FX in
+    // the workspace (the restoration problem's own region)
+    MPCG_HD int fx_off() const { return RESTO ? L.SP_FLTR() : L.SP_FLT(); }
+    MPCG_HD void fget(int f, T& th, T& ph) const {
+        if (f < L.cap) {
+            th = ld(L.FI() + 2 * f);
+            ph = ld(L.FI() + 2 * f + 1);
+        } else {
+            const T* x = spill + fx_off() + 2 * (f - L.cap);
+            th = x[0];
+            ph = x[1];
+        }
+    }
+    MPCG_HD void fset(int f, T th, T ph) const {
+        if (f < L.cap) {
+            st(L.FI() + 2 * f, th);
+            st(L.FI() + 2 * f + 1, ph);
+        } else {
+            T* x = spill + fx_off() + 2 * (f - L.cap);
+            x[0] = th;
+            x[1] = ph;
+        }
+    }
     // acceptable to the filter: no entry f with theta >= theta_f and phi >= phi_f (lane f tests entry f)
     MPCG_HD bool filter_ok(T phit, T thetat) {
         const int t = wv.lane();
-        const int fi = L.FI();
         bool hit = false;
         for (int f0 = 0; f0 < nf; f0 += 64) {
             const int f = f0 + t;
-            const bool h = f < nf && thetat >= ld(fi + 2 * f) && phit >= ld(fi + 2 * f + 1);
+            T e0 = 0, e1 = 0;
+            if (f < nf) fget(f, e0, e1);
+            const bool h = f < nf && thetat >= e0 && phit >= e1;
             hit = hit || wv.any(h);
         }
         return !hit;
     }
     // Filter::AddEntry: the entries the new one dominates are dropped (acceptance does not
-    // change); beyond filter_cap non-dominated entries the oldest is dropped
+    // change); the filter holds filter_cap + WideLayout::FX entries, beyond which the oldest
+    // is dropped and counted (n_fover)
     MPCG_HD void filter_add(T ph, T th) {
         const int t = wv.lane();
-        const int fi = L.FI(), cap = P.filter_cap;
+        const int cap = L.cap + WideLayout::FX;
+        const bool ext = nf > L.cap;  // (entries in the workspace: cross-lane global-memory order)
         int base = 0;
         for (int f0 = 0; f0 < nf; f0 += 64) {
             const int f = f0 + t;
             T e0 = 0, e1 = 0;
             wv.sync();
-            if (f < nf) {
-                e0 = ld(fi + 2 * f);
-                e1 = ld(fi + 2 * f + 1);
-            }
+            if (f < nf) fget(f, e0, e1);
             const bool keep = f < nf && !(ph <= e1 && th <= e0);
             int cnt;
             const int dst = base + wv.ballot_prefix(keep, &cnt);
             wv.sync();
-            if (keep) {
-                st(fi + 2 * dst, e0);
-                st(fi + 2 * dst + 1, e1);
-            }
+            if (ext) wv.gsync();
+            if (keep) fset(dst, e0, e1);
             base += cnt;
         }
         nf = wv.uni(base);
         int slot = nf;
         if (nf == cap) {  // full: drop the oldest entry
+            ++n_fover;
             T e0 = 0, e1 = 0;
             for (int f0 = 0; f0 < cap; f0 += 64) {
                 const int f = f0 + t + 1;
                 wv.sync();
-                if (f < cap) { e0 = ld(fi + 2 * f); e1 = ld(fi + 2 * f + 1); }
+                wv.gsync();
+                if (f < cap) fget(f, e0, e1);
                 wv.sync();
-                if (f < cap) { st(fi + 2 * (f - 1), e0); st(fi + 2 * (f - 1) + 1, e1); }
+                wv.gsync();
+                if (f < cap) fset(f - 1, e0, e1);
             }
             slot = cap - 1;
         } else {
             ++nf;
+            nf_peak = nf > nf_peak ? nf : nf_peak;
         }
         wv.sync();
-        if (t == 0) {
-            st(fi + 2 * slot, th);
-            st(fi + 2 * slot + 1, ph);
-        }
+        if (t == 0) fset(slot, th, ph);
         wv.sync();
+        if (nf > L.cap) wv.gsync();
     }
     MPCG_HD void augment_filter() {
         filter_add(ref_phi - (T)1e-8 * ref_theta, ((T)1 - (T)1e-5) * ref_theta);
@@ -3681,6 +3714,7 @@ struct WideSolver {
     // the image comes back with the new iterate (x of the restoration problem, y = 0, the
     // bound multipliers of its step), which AcceptTrialPoint takes as the next iterate.
     MPCG_HD int restoration() {
+        ++n_resto;
         spill_out(L.SP_DUMP(), 0, L.total());
         wv.gsync();
         const RestoIn<T> in{mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, nf, iter};
@@ -3689,6 +3723,7 @@ struct WideSolver {
         wv.gsync();
         spill_in(L.SP_DUMP(), 0, L.total());
         iter = wv.uni(o.iter);
+        n_fover += wv.uni(o.fover);
         c_ok = 0;
         const int s = wv.uni(o.status);
         if (s) return s;
@@ -3755,9 +3790,9 @@ struct WideSolver {
         run();
         if (status == RESTO_DONE) {
             resto_finish();
-            return RestoOut{0, iter};
+            return RestoOut{0, iter, n_fover};
         }
-        return RestoOut{status, iter};
+        return RestoOut{status, iter, n_fover};
     }
 
     // RestoConvergenceCheck / RestoFilterConvergenceCheck::TestOrigProgress (from the second
@@ -3845,7 +3880,13 @@ struct WideSolver {
         bool hit = false;
         for (int f0 = 0; f0 < o_nf; f0 += 64) {
             const int f = f0 + t;
-            const bool h = f < o_nf && r_thO >= dumpO[fi + 2 * f] && r_phiO >= dumpO[fi + 2 * f + 1];
+            T e0 = 0, e1 = 0;
+            if (f < o_nf) {
+                const T* x = f < L.cap ? dumpO + fi + 2 * f : spill + L.SP_FLT() + 2 * (f - L.cap);
+                e0 = x[0];
+                e1 = x[1];
+            }
+            const bool h = f < o_nf && r_thO >= e0 && r_phiO >= e1;
             hit = hit || wv.any(h);
         }
         if (hit) return false;
@@ -3960,16 +4001,17 @@ struct WideSolver {
         const int t = wv.lane();
         wv.sync();
         if (t == 0) {
-            const T v[24] = {mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, theta_min, dw_last, delta_w_used,
+            const T v[27] = {mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, theta_min, dw_last, delta_w_used,
                              (T)iter, (T)nf, (T)last_rej_filter, (T)count_filter_rej, (T)n_filter_resets,
                              (T)tiny_last, (T)tiny_flag, (T)acc_counter, (T)have_acc, (T)in_wd, (T)wd_short,
-                             (T)in_soft, (T)soft_count, (T)wd_trial_iter};
-            for (int i = 0; i < 24; ++i) dst[i] = v[i];
+                             (T)in_soft, (T)soft_count, (T)wd_trial_iter, (T)n_fover, (T)n_resto, (T)nf_peak};
+            for (int i = 0; i < 27; ++i) dst[i] = v[i];
         }
         T* img = dst + PARK_SCALARS;
         for (int e = t; e < L.total(); e += 64) img[e] = ld(e);
-        T* acc = img + L.total() + L.SP_ACC();
-        for (int e = t; e < WideLayout::WS * N; e += 64) acc[e] = spill[L.SP_ACC() + e];
+        T* ws = img + L.total();  // (the acceptable point and the filter's workspace entries)
+        for (int e = t; e < WideLayout::WS * N; e += 64) ws[L.SP_ACC() + e] = spill[L.SP_ACC() + e];
+        for (int e = t; e < 2 * WideLayout::FX; e += 64) ws[L.SP_FLT() + e] = spill[L.SP_FLT() + e];
     }
     // (the solver constructed with spill = park_entry + PARK_SCALARS + total())
     MPCG_HD void unpark(const T* src) {
@@ -4003,6 +4045,9 @@ struct WideSolver {
         in_soft = wv.uni((int)src[21]);
         soft_count = wv.uni((int)src[22]);
         wd_trial_iter = wv.uni((int)src[23]);
+        n_fover = wv.uni((int)src[24]);
+        n_resto = wv.uni((int)src[25]);
+        nf_peak = wv.uni((int)src[26]);
         status = NEED_RESTO;
         c_ok = 0;
         acc_pending = false;

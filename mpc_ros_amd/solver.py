@@ -93,16 +93,19 @@ class BatchSolver:
         status = np.zeros(B, dtype=np.int32)
         iters = np.zeros(B, dtype=np.int32)
         obj = np.zeros(B)
+        diag = np.zeros((B, 4), dtype=np.int32)
         dp = C.POINTER(C.c_double)
         ip = C.POINTER(C.c_int32)
-        _lib.check(_lib.lib().mpcg_solve(
+        _lib.check(_lib.lib().mpcg_solve_ex(
             self._h, B, state.ctypes.data_as(dp), coeffs.ctypes.data_as(dp), u0.ctypes.data_as(dp),
             traj.ctypes.data_as(dp) if traj is not None else None, status.ctypes.data_as(ip),
-            obj.ctypes.data_as(dp), iters.ctypes.data_as(ip)), "mpcg_solve")
-        return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters)
+            obj.ctypes.data_as(dp), iters.ctypes.data_as(ip), diag.ctypes.data_as(ip)), "mpcg_solve_ex")
+        # diag columns: restoration phases, filter entries dropped beyond its capacity, parked, 0
+        return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters, diag=diag)
 
-    def solve_device(self, state, coeffs, u0, traj=None, status=None, obj=None, iters=None, stream=None):
-        """All arguments are torch tensors on this handle's GPU (float64 / int32, contiguous)."""
+    def solve_device(self, state, coeffs, u0, traj=None, status=None, obj=None, iters=None, stream=None, diag=None):
+        """All arguments are torch tensors on this handle's GPU (float64 / int32, contiguous);
+        diag [B, 4] int32: restoration phases, filter overflows, parked, 0."""
         import torch
 
         B = state.shape[0]
@@ -113,12 +116,13 @@ class BatchSolver:
             assert traj.dtype == torch.float64 and traj.is_contiguous() and traj.numel() == B * 3 * self.N
         for t in (status, iters):
             assert t is None or (t.dtype == torch.int32 and t.numel() == B)
+        assert diag is None or (diag.dtype == torch.int32 and diag.numel() == 4 * B and diag.is_contiguous())
         if stream is None:
             stream = torch.cuda.current_stream(state.device)
         ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-        _lib.check(_lib.lib().mpcg_solve_device(
-            self._h, B, ptr(state), ptr(coeffs), ptr(u0), ptr(traj), ptr(status), ptr(obj), ptr(iters),
-            C.c_void_p(stream.cuda_stream)), "mpcg_solve_device")
+        _lib.check(_lib.lib().mpcg_solve_device_ex(
+            self._h, B, ptr(state), ptr(coeffs), ptr(u0), ptr(traj), ptr(status), ptr(obj), ptr(iters), ptr(diag),
+            C.c_void_p(stream.cuda_stream)), "mpcg_solve_device_ex")
 
     # ------------------------------------------------ the caller side on the device
     def preprocess_device(self, pose, vel, plan, state, coeffs, delay_mode: bool = True, stream=None):

@@ -14,7 +14,7 @@
 //         filter_reset_trigger tiny_step_tol tiny_step_y_tol cpu_iter_budget filter_cap
 //         dual_inf_tol constr_viol_tol compl_inf_tol
 //         B, then B x (state[6], coeffs[4])
-// stdout: per problem: status iters obj u0[2] traj[3N]
+// stdout: per problem: status iters obj u0[2] traj[3N] restoration-phases filter-overflows filter-peak
 #include <barrier>
 #include <type_traits>
 #include <cmath>
@@ -171,7 +171,7 @@ int main() {
         sh.lds.assign(L.total(), std::nan(""));
         std::vector<HT> spill(L.slot(), (HT)std::nan(""));
         std::vector<HT> park(32 + L.total() + L.slot(), (HT)std::nan(""));
-        int status = 0, iters = 0;
+        int status = 0, iters = 0, nresto = 0, nfover = 0, nfpeak = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
         std::vector<std::thread> th;
@@ -195,6 +195,9 @@ int main() {
                     if (t == 0) {
                         status = S.status;
                         iters = S.iter;
+                        nresto = S.n_resto;
+                        nfover = S.n_fover;
+                        nfpeak = S.nf_peak;
                         obj = o;
                         u0 = S.x_ctrl(0, 0);
                         u1 = S.x_ctrl(1, 0);
@@ -226,7 +229,7 @@ int main() {
         for (auto& x : th) x.join();
         std::printf("%d %d %.17g %.17g %.17g", status, iters, obj, u0, u1);
         for (double v : traj) std::printf(" %.17g", v);
-        std::printf("\n");
+        std::printf(" %d %d %d\n", nresto, nfover, nfpeak);
     }
     return 0;
 }

@@ -53,12 +53,18 @@ def run_harness(exe, P, state, coeffs, opts=None):
     out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True).stdout
     rows = np.array([r.split() for r in out.strip().split("\n")], dtype=np.float64)
     return dict(status=rows[:, 0].astype(int), iters=rows[:, 1].astype(int), obj=rows[:, 2], u0=rows[:, 3:5],
-                traj=rows[:, 5:].reshape(len(state), 3, N))
+                traj=rows[:, 5:5 + 3 * N].reshape(len(state), 3, N), n_resto=rows[:, 5 + 3 * N].astype(int),
+                n_fover=rows[:, 6 + 3 * N].astype(int), nf_peak=rows[:, 7 + 3 * N].astype(int))
 
 
 def compare(r, g, atol=1e-9):
     """Same status and iteration count, values to rounding -- every row, including those
-    on which the oracle runs Ipopt's feasibility-restoration phase (diag[:, 3] > 0)."""
+    on which the oracle runs Ipopt's feasibility-restoration phase (diag[:, 3] > 0), the same
+    number of restoration phases, and no filter entry dropped (Ipopt's filter is unbounded)."""
+    if "diag" in g and "n_resto" in r:
+        np.testing.assert_array_equal(r["n_resto"], g["diag"][:, 3])
+    if "n_fover" in r:
+        assert (r["n_fover"] == 0).all()
     np.testing.assert_array_equal(r["status"], g["status"])
     np.testing.assert_array_equal(r["iters"], g["iters"])
     np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=atol)
@@ -98,6 +104,23 @@ def test_wide_core_ipopt_features(wide_harness, features_golden, name):
     sub = subset(g, rows)
     r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
     compare(r, sub, atol=1e-9)
+
+
+# The most filter entries held at once (diag[:, 3] on the device) on the round-1 advisor's
+# filter problems (N20 set) and on resto_N40's 19304, whose filter reaches 196 entries:
+# beyond the 64 in LDS, in the workspace extension (WideLayout::FX), none dropped.
+FILTER_PEAKS = {"N20": {1887: 53, 16101: 51}, "resto_N40": {19304: 196}}
+
+
+def test_wide_core_filter_beyond_lds(wide_harness, features_golden):
+    for name, peaks in FILTER_PEAKS.items():
+        g = features_golden[name]
+        rows = [int(np.flatnonzero(g["index"] == pid)[0]) for pid in peaks]
+        sub = {k: g[k][rows] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
+        r = run_harness(wide_harness, g["P"], sub["state"], sub["coeffs"])
+        compare(r, sub, atol=1e-7)
+        np.testing.assert_array_equal(r["nf_peak"], list(peaks.values()))
+        assert (r["n_fover"] == 0).all()
 
 
 @pytest.mark.parametrize("name", ["resto_N20", "resto_N40"])

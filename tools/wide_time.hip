@@ -84,7 +84,7 @@ int main(int argc, char** argv) {
 #ifdef WT_OLD_API
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill, 0));
 #else
-        CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill,
+        CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, nullptr, order, dspill,
                                    mpcg::wide_spill_bytes(P, B), 0, getenv("WT_SEQ") ? nullptr : aux, evf, evj));
 #endif
         CK(hipEventRecord(e1));
