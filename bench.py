@@ -11,21 +11,22 @@ equal --gpus (a mismatch is an error, never a silently smaller run).
 A step = one pass of the hot path over one batch: every rank solves its shard of
 B problems (BASELINE.json configs[3]: 524288 problems over 8 GPUs = 65536 per GPU,
 N = 20, fp64, differential drive) with the HIP kernel, then the controls and
-statuses are gathered to rank 0 (RCCL all-gather over xGMI) -- the only
-collective.  Inputs are resident in HBM before the timed region (weak scaling: the
+statuses are gathered to rank 0 (torch.distributed.gather: RCCL point-to-point over
+xGMI, each rank sends its slice only) -- the only exchange.  Inputs are resident in HBM before the timed region (weak scaling: the
 per-GPU batch is fixed).  Rank 0 prints one JSON line.
 
-roofline: the dominant (only) kernel, mpcg::k_solve_wide (one problem per
-wavefront, whole problem state in LDS).  achieved = algorithmic bytes per launch
-(B x 8 x (6 + 4 + 2 + 3N) = B x 576 B at N = 20) divided by the
-kernel's average duration measured with HIP events on the stream it runs on;
-traffic = memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the committed
-rocprofv3 PMC summary for this configuration (profiles/pmc_B<B>_N<N>.json), or null.
-The path is not HBM-bound: the kernel is FP64-VALU issue/latency
-bound, so the line also carries valu_fp64 = FP64 FLOP/s (PMC-counted FLOPs per
-solve x solves / kernel time: physical lane-FLOPs, redundant lanes included) and
-valu_algorithmic = the useful flops of SURVEY.md §8d's formula (iterations x Riccati
-and forward-pass flops per stage) / kernel time, both against the vector peak.
+roofline: the dominant kernel, mpcg::k_solve_wide (one problem per wavefront, whole
+problem state in LDS; the restoration phase's k_resume_wide runs beside it on a second
+stream and both are inside the timed events).  The path is not HBM-bound (SURVEY.md
+§8d): it is FP64 vector-ALU issue/latency bound, so bound = "valu_fp64" and achieved =
+the useful flops of SURVEY.md §8d's formula (iterations x Riccati and forward-pass flops
+per stage, per solve) x the solves of one launch / the launch's average duration
+(HIP events on the stream it runs on), against the FP64 vector peak.  traffic =
+memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3 PMC
+summary of this exact configuration (profiles/r3/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json),
+or null.  The line also carries hbm = algorithmic bytes per launch (B x 8 x (6 + 4 + 2 +
+3N) = B x 576 B at N = 20) / kernel time against 8 TB/s, and valu_fp64 = PMC-counted
+FP64 lane-FLOPs (redundant lanes included) / kernel time.
 cpu_baseline: the oracle (the Ipopt restatement, "port") on a bounded sample of the
 same problems, rank 0, N = 1 only: its KKT systems in stage order factored within their
 band (the structured linear algebra, as Ipopt's sparse solver would) as the value, the
@@ -69,8 +70,8 @@ def parse():
     ap.add_argument("--gather-traj", action="store_true", help="also gather the 3N trajectories")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--profile-name", default=None, help="PMC summary to read traffic from")
-    ap.add_argument("--strategy", default="auto", choices=["auto", "lane", "wave"],
-                    help="kernel strategy: one problem per lane / per wavefront")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "wave"],
+                    help="kernel strategy: one problem per wavefront (the only one)")
     ap.add_argument("--model", default="diffdrive", choices=["diffdrive", "bicycle"],
                     help="dynamics: FG_eval's differential drive, or the kinematic bicycle (BASELINE configs[4]: "
                          "run with --horizon 25)")
@@ -173,6 +174,11 @@ def latency_b1(P, st, cf, solver, dev, reps=50):
     return {"gpu_device_ms": float(np.median(dev_ms)), "gpu_host_buffers_ms": float(np.median(host_ms)),
             "cpu_oracle_ms": float(np.median(cpu_ms)),
             "sample": f"problem 0 of the batch, B = 1, median of {reps} (GPU) / {min(reps, 20)} (CPU, 1 thread)"}
+
+
+def pmc_name(a) -> str:
+    """The PMC summary of exactly this configuration (model, mode, dtype, batch, horizon)."""
+    return a.profile_name or f"r3/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}"
 
 
 def pmc_profile(name):
@@ -297,6 +303,7 @@ def main():
     traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)
     status = torch.empty(count, dtype=torch.int32, device=dev)
     iters = torch.empty(count, dtype=torch.int32, device=dev)
+    diag = torch.zeros((count, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     k_ms = []
 
@@ -309,7 +316,7 @@ def main():
         if a.mode == "track":
             solver.track_device(tpose, tvel, tplan, cmd, traj, status, stream=stream)
         else:
-            solver.solve_device(tst, tcf, u0, traj, status, None, iters, stream=stream)
+            solver.solve_device(tst, tcf, u0, traj, status, None, iters, stream=stream, diag=diag)
         if timed:
             e1.record(stream)
             k_ms.append((e0, e1))
@@ -349,16 +356,28 @@ def main():
         per_rank = {"kernel_ms": allr[:, 1].tolist(), "gather_ms": allr[:, 2].tolist()}
         elapsed, kern, gath = float(allr[:, 0].max()), float(allr[:, 1].max()), float(allr[:, 2].max())
     if a.mode == "track":  # iteration counts of the same problems
-        solver.solve_device(tst, tcf, u0, None, None, None, iters, stream=stream)
+        solver.solve_device(tst, tcf, u0, None, status, None, iters, stream=stream, diag=diag)
         torch.cuda.synchronize()
     it = iters.cpu().numpy()
     sts = status.cpu().numpy()
+    dg = diag.cpu().numpy()
+    # (per-rank status and diagnostic counts, summed over ranks)
+    codes = list(range(16))
+    mine = torch.tensor([int(np.sum(sts == c)) for c in codes] +
+                        [int(np.sum(dg[:, 0] > 0)), int(dg[:, 0].sum()), int(dg[:, 2].sum()), int(np.sum(dg[:, 1] > 0)),
+                         int(dg[:, 3].max(initial=0))], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(mine[:-1])
+        peak = mine[-1:].clone()
+        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+        mine[-1:] = peak
+    cnt = mine.cpu().numpy()
     if rank == 0:
         value = total * a.steps / elapsed
         bytes_per_solve = 8 * (6 + 4 + 2 + 3 * N)
         achieved = count * bytes_per_solve / (kern * 1e-3) / 1e9
-        prof = a.profile_name or f"pmc_B{B}_N{N}"
-        pmc = pmc_profile(prof) if a.dtype == "fp64" else {}
+        prof = pmc_name(a)
+        pmc = pmc_profile(prof)
         traffic = pmc.get("hbm_bytes_per_launch")
         fl = pmc.get("fp64_flops_per_solve")
         valu = None
@@ -393,15 +412,20 @@ def main():
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
                        "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}",
                        "mode": a.mode, "model": a.model, "dtype": a.dtype},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mpcg::k_solve_wide" if solver.strategy == "wave" else "lane kernels",
-                         "strategy": solver.strategy, "kernel_ms": kern,
-                         "algorithmic_bytes_per_solve": bytes_per_solve,
+            "roofline": {"bound": "valu_fp64" if a.dtype == "fp64" else "valu_fp32", "achieved": got_a,
+                         "peak": peak_a, "unit": "TFLOP/s", "frac": got_a / peak_a, "traffic": traffic,
+                         "kernel": "mpcg::k_solve_wide", "kernel_ms": kern,
+                         "algorithmic_flops_per_solve": af, "solves_per_launch": count,
                          "traffic_source": f"profiles/{prof}.json" if traffic else None,
+                         "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_solve": bytes_per_solve},
                          "valu_fp64": valu, "valu_algorithmic": valu_alg},
             "solver": {"iters_mean": float(it.mean()), "iters_max": int(it.max()),
-                       "success_frac": float(np.mean(sts == 1))},
+                       "success_frac": float(cnt[1] / total),
+                       "status_counts": {str(c): int(cnt[c]) for c in codes if cnt[c]},
+                       "restoration": {"problems": int(cnt[16]), "phases": int(cnt[17]), "parked": int(cnt[18])},
+                       "filter": {"problems_dropping_entries": int(cnt[19]), "peak_entries": int(cnt[20])},
+                       "sample": "all problems of the last timed step, all ranks"},
             "timing": {"kernel_ms": kern, "gather_ms": gath, "per_rank": per_rank},
         }
         if world == 1 and a.cpu_seconds > 0:

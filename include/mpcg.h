@@ -159,7 +159,7 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
  * may be NULL): restoration phases entered, filter entries dropped beyond its capacity
  * (filter_cap in LDS plus 448 in the workspace; Ipopt's filter is unbounded, so any nonzero
  * value marks a solve that may differ from Ipopt's), 1 if the problem was continued by the
- * parked-problem kernel, 0. */
+ * parked-problem kernel, the most filter entries held at once (the original problem). */
 int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
                   int32_t* status, double* obj, int32_t* iters, int32_t* diag);
 int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
@@ -172,9 +172,26 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
  * gathered to devices[0] by grouped RCCL send/recv (one message per output array and GPU,
  * point-to-point over xGMI), then copied to the host.  Creates and destroys its handles and
  * communicator per call (a serving loop keeps per-GPU handles and gathers itself, as
- * bench.py does with torch.distributed).  Returns 0, or < 0 (-4: RCCL). */
+ * bench.py does with torch.distributed).  Returns 0, or < 0 with mpcg_last_error() set
+ * (-1 arguments, -2 HIP, -3 device ordinal, -4 RCCL). */
 int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
                      const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters);
+
+/* mpcg_solve_multi's arithmetic, pure functions (no GPU):
+ * mpcg_shard_range: GPU r of ngpu solves problems [start, start + count) -- contiguous,
+ *   the first B % ngpu GPUs one more, empty shards when B < ngpu.
+ * mpcg_multi_gather_plan: the MPCG_GATHER_ARRAYS messages GPU r sends to devices[0]
+ *   (u0, traj, obj, status, iters): byte offsets in its own output buffer and in the root's
+ *   gathered buffer of mpcg_multi_out_bytes(B, N) bytes, and sizes (count x 32 + 24 N bytes
+ *   in all; 0 for an empty shard).  For r = 0 src_offset == dst_offset: the root solves in
+ *   place and sends nothing. */
+#define MPCG_GATHER_ARRAYS 5
+typedef struct mpcg_xfer {
+    size_t src_offset, dst_offset, bytes;
+} mpcg_xfer;
+int mpcg_shard_range(int64_t B, int ngpu, int r, int64_t* start, int64_t* count);
+int mpcg_multi_gather_plan(int64_t B, int32_t N, int ngpu, int r, mpcg_xfer* xfers);
+size_t mpcg_multi_out_bytes(int64_t B, int32_t N);
 
 /* Tracking::findBestPath's preprocessing (mpc_ros/src/driving_state.cpp:175-256) on the
  * device for B robots: waypoints to the vehicle frame, cubic polyfit (Householder QR),

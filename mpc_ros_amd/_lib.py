@@ -45,6 +45,14 @@ class MpcgParams(C.Structure):
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
 _PP = C.POINTER(MpcgParams)
+
+
+class MpcgXfer(C.Structure):
+    """mpcg_xfer (include/mpcg.h): one gather message of mpcg_solve_multi."""
+    _fields_ = [("src_offset", C.c_size_t), ("dst_offset", C.c_size_t), ("bytes", C.c_size_t)]
+
+
+GATHER_ARRAYS = 5  # MPCG_GATHER_ARRAYS
 SIGNATURES = {
     "mpcg_abi_version": ([], C.c_int),
     "mpcg_build_id": ([], C.c_char_p),
@@ -71,6 +79,9 @@ SIGNATURES = {
                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mpcg_synchronize": ([C.c_void_p], C.c_int),
     "mpcg_solve_multi": ([C.c_int, C.POINTER(C.c_int), _PP, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip], C.c_int),
+    "mpcg_shard_range": ([C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
+    "mpcg_multi_gather_plan": ([C.c_int64, C.c_int32, C.c_int, C.c_int, C.c_void_p], C.c_int),
+    "mpcg_multi_out_bytes": ([C.c_int64, C.c_int32], C.c_size_t),
     "mpcg_set_strategy": ([C.c_void_p, C.c_int32], C.c_int),
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
 }

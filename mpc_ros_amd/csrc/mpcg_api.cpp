@@ -15,11 +15,17 @@
 
 namespace {
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+namespace mpcg {
+int set_error(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace mpcg
+
+namespace {
+int fail(int code, const std::string& msg) { return mpcg::set_error(code, msg); }
 int hip_fail(hipError_t e, const char* what) {
     return fail(-2, std::string(what) + ": " + hipGetErrorString(e));
 }

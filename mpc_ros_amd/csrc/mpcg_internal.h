@@ -5,9 +5,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "ipm_core.h"
 
 namespace mpcg {
+
+// mpcg_last_error()'s message for this thread; returns code
+int set_error(int code, const std::string& msg);
 
 // One problem per wavefront (mpcg_wide.hip): LDS bytes per problem, launch.
 size_t wide_lds_bytes(const IpmParams& P);

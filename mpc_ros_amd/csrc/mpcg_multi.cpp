@@ -1,11 +1,13 @@
 // mpc_ros_amd/csrc/mpcg_multi.cpp -- mpcg_solve_multi: one process, several GPUs, RCCL gather.
 //
 // the B problems are independent, so they are split into contiguous
-// shards (the first B % G GPUs take one extra problem), each GPU solves its shard with
-// its own handle and stream, and the per-problem results are gathered to the first GPU
-// with one grouped RCCL send/recv per output array (rank r sends its shard, the root
-// receives every shard at its offset: point-to-point over xGMI, the north star's "RCCL
-// used only for the final gather"), then copied to the caller's host buffers.
+// shards (mpcg_shard_range: the first B % G GPUs take one extra problem), each GPU solves
+// its shard with its own handle and stream, and the per-problem results are gathered to
+// the first GPU with one grouped RCCL send/recv per output array (mpcg_multi_gather_plan:
+// rank r sends its shard, the root receives every shard at its offset -- point-to-point
+// over xGMI, the north star's "RCCL used only for the final gather"), then copied to the
+// caller's host buffers.  Every HIP and RCCL return is checked; a failure sets
+// mpcg_last_error() and the call drains its streams before it frees anything.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -14,6 +16,7 @@
 #include <vector>
 
 #include "mpcg.h"
+#include "mpcg_internal.h"
 
 namespace {
 struct Shard {
@@ -22,8 +25,7 @@ struct Shard {
     hipStream_t s = nullptr;
     int64_t start = 0, count = 0;
     double* in = nullptr;   // state [count][6] | coeffs [count][4]
-    double* out = nullptr;  // root: gathered outputs of all B problems; others: their shard
-    size_t out_bytes = 0;
+    char* out = nullptr;    // root: gathered outputs of all B problems; others: their shard
 };
 
 // output record layout of B problems: u0 [B][2] | traj [B][3N] | obj [B] | status [B] | iters [B]
@@ -37,30 +39,78 @@ struct OutLayout {
     size_t iters() const { return status() + sizeof(int32_t) * B; }
     size_t total() const { return iters() + sizeof(int32_t) * B; }
 };
+
+int nccl_fail(ncclResult_t e, const char* what) {
+    return mpcg::set_error(-4, std::string(what) + ": " + ncclGetErrorString(e));
+}
+int hip_fail(hipError_t e, const char* what) {
+    return mpcg::set_error(-2, std::string(what) + ": " + hipGetErrorString(e));
+}
 }  // namespace
 
-extern "C" int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B,
-                                const double* state, const double* coeffs, double* u0, double* traj,
-                                int32_t* status, double* obj, int32_t* iters) {
-    if (ngpu < 1 || !devices || !params) return -1;
-    if (B < 0) return -1;
+extern "C" {
+
+int mpcg_shard_range(int64_t B, int ngpu, int r, int64_t* start, int64_t* count) {
+    if (B < 0 || ngpu < 1 || r < 0 || r >= ngpu || !start || !count)
+        return mpcg::set_error(-1, "mpcg_shard_range: B >= 0, 0 <= r < ngpu and non-null outputs");
+    const int64_t base = B / ngpu, rem = B % ngpu;
+    *count = base + (r < rem ? 1 : 0);
+    *start = r * base + (r < rem ? r : rem);
+    return 0;
+}
+
+int mpcg_multi_gather_plan(int64_t B, int32_t N, int ngpu, int r, mpcg_xfer* xfers) {
+    if (N < 1 || !xfers) return mpcg::set_error(-1, "mpcg_multi_gather_plan: N >= 1 and non-null xfers");
+    int64_t start = 0, count = 0;
+    if (int rc = mpcg_shard_range(B, ngpu, r, &start, &count)) return rc;
+    const OutLayout G{B, N}, L{r == 0 ? B : count, N};
+    // rank 0 solves in place into its slot of the gathered arrays (src == dst, nothing moves)
+    const int64_t so = r == 0 ? start : 0;
+    const size_t src[MPCG_GATHER_ARRAYS] = {L.u0(), L.traj(), L.obj(), L.status(), L.iters()};
+    const size_t dst[MPCG_GATHER_ARRAYS] = {G.u0(), G.traj(), G.obj(), G.status(), G.iters()};
+    const size_t per[MPCG_GATHER_ARRAYS] = {sizeof(double) * 2, sizeof(double) * 3 * (size_t)N, sizeof(double),
+                                            sizeof(int32_t), sizeof(int32_t)};
+    for (int k = 0; k < MPCG_GATHER_ARRAYS; ++k) {
+        xfers[k].src_offset = src[k] + per[k] * (size_t)so;
+        xfers[k].dst_offset = dst[k] + per[k] * (size_t)start;
+        xfers[k].bytes = per[k] * (size_t)count;
+    }
+    return 0;
+}
+
+size_t mpcg_multi_out_bytes(int64_t B, int32_t N) {
+    return B < 0 || N < 1 ? 0 : OutLayout{B, N}.total();
+}
+
+int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
+                     const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters) {
+    if (ngpu < 1 || !devices || !params) return mpcg::set_error(-1, "mpcg_solve_multi: ngpu >= 1, devices, params");
+    if (B < 0) return mpcg::set_error(-1, "mpcg_solve_multi: B < 0");
     if (B == 0) return 0;
-    if (!state || !coeffs || !u0) return -1;
+    if (!state || !coeffs || !u0) return mpcg::set_error(-1, "mpcg_solve_multi: null state / coeffs / u0");
     int rc = mpcg_params_check(params);
     if (rc) return rc;
+    int ndev = 0;
+    hipError_t he = hipGetDeviceCount(&ndev);
+    if (he != hipSuccess) return hip_fail(he, "hipGetDeviceCount");
+    for (int r = 0; r < ngpu; ++r) {
+        if (devices[r] < 0 || devices[r] >= ndev) return mpcg::set_error(-3, "mpcg_solve_multi: device out of range");
+        for (int q = 0; q < r; ++q)
+            if (devices[q] == devices[r]) return mpcg::set_error(-1, "mpcg_solve_multi: devices repeat");
+    }
     const int N = params->steps;
     std::vector<Shard> sh(ngpu);
-    const int64_t base = B / ngpu, rem = B % ngpu;
     for (int r = 0; r < ngpu; ++r) {
         sh[r].dev = devices[r];
-        sh[r].count = base + (r < rem ? 1 : 0);
-        sh[r].start = r * base + (r < rem ? r : rem);
+        mpcg_shard_range(B, ngpu, r, &sh[r].start, &sh[r].count);
     }
     std::vector<ncclComm_t> comms(ngpu, nullptr);
+    // (drains every stream before it frees: a failure may leave work queued)
     auto cleanup = [&]() {
         for (auto& s : sh) {
-            if (s.h) mpcg_destroy(s.h);
             hipSetDevice(s.dev);
+            if (s.s) hipStreamSynchronize(s.s);
+            if (s.h) mpcg_destroy(s.h);
             if (s.in) hipFree(s.in);
             if (s.out) hipFree(s.out);
             if (s.s) hipStreamDestroy(s.s);
@@ -70,69 +120,93 @@ extern "C" int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params*
     };
     int result = 0;
     do {
-        if (ncclCommInitAll(comms.data(), ngpu, devices) != ncclSuccess) { result = -4; break; }
+        ncclResult_t ne = ncclCommInitAll(comms.data(), ngpu, devices);
+        if (ne != ncclSuccess) { result = nccl_fail(ne, "ncclCommInitAll"); break; }
         // shards: copy in, solve (each on its own GPU and stream, queued without waiting)
         for (int r = 0; r < ngpu && !result; ++r) {
             Shard& s = sh[r];
             if ((rc = mpcg_create(s.dev, &s.h)) != 0) { result = rc; break; }
             if ((rc = mpcg_set_params(s.h, params)) != 0) { result = rc; break; }
-            hipSetDevice(s.dev);
-            if (hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking) != hipSuccess) { result = -2; break; }
-            const OutLayout L{r == 0 ? B : s.count, N};
-            s.out_bytes = L.total();
-            if (hipMalloc((void**)&s.in, sizeof(double) * 10 * (s.count > 0 ? s.count : 1)) != hipSuccess ||
-                hipMalloc((void**)&s.out, s.out_bytes) != hipSuccess) { result = -2; break; }
+            if ((he = hipSetDevice(s.dev)) != hipSuccess) { result = hip_fail(he, "hipSetDevice"); break; }
+            if ((he = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking)) != hipSuccess) {
+                result = hip_fail(he, "hipStreamCreateWithFlags");
+                break;
+            }
+            const size_t out_bytes = OutLayout{r == 0 ? B : s.count, N}.total();
+            if ((he = hipMalloc((void**)&s.in, sizeof(double) * 10 * (s.count > 0 ? s.count : 1))) != hipSuccess ||
+                (he = hipMalloc((void**)&s.out, out_bytes > 0 ? out_bytes : 1)) != hipSuccess) {
+                result = hip_fail(he, "hipMalloc");
+                break;
+            }
             if (s.count == 0) continue;
             double* din = s.in;
-            hipMemcpyAsync(din, state + 6 * s.start, sizeof(double) * 6 * s.count, hipMemcpyHostToDevice, s.s);
-            hipMemcpyAsync(din + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count,
-                           hipMemcpyHostToDevice, s.s);
-            // the root solves into its own slot of the gathered arrays
-            const OutLayout G{B, N};
-            char* o = (char*)s.out;
-            const int64_t off = r == 0 ? s.start : 0;
-            const OutLayout& Lr = r == 0 ? G : L;
-            rc = mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + Lr.u0()) + 2 * off,
-                                   (double*)(o + Lr.traj()) + (size_t)3 * N * off, (int32_t*)(o + Lr.status()) + off,
-                                   (double*)(o + Lr.obj()) + off, (int32_t*)(o + Lr.iters()) + off, s.s);
+            if ((he = hipMemcpyAsync(din, state + 6 * s.start, sizeof(double) * 6 * s.count, hipMemcpyHostToDevice,
+                                     s.s)) != hipSuccess ||
+                (he = hipMemcpyAsync(din + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count,
+                                     hipMemcpyHostToDevice, s.s)) != hipSuccess) {
+                result = hip_fail(he, "hipMemcpyAsync (inputs)");
+                break;
+            }
+            // the root solves into its own slot of the gathered arrays (the plan's src offsets)
+            mpcg_xfer x[MPCG_GATHER_ARRAYS];
+            if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) { result = rc; break; }
+            char* o = s.out;
+            rc = mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + x[0].src_offset),
+                                   (double*)(o + x[1].src_offset), (int32_t*)(o + x[3].src_offset),
+                                   (double*)(o + x[2].src_offset), (int32_t*)(o + x[4].src_offset), s.s);
             if (rc) { result = rc; break; }
         }
         if (result) break;
-        // the gather: rank r > 0 sends each of its output arrays, the root receives them
-        // at their offsets (grouped point-to-point: every shard moves once over xGMI)
-        const OutLayout G{B, N};
-        if (ncclGroupStart() != ncclSuccess) { result = -4; break; }
-        for (int r = 1; r < ngpu; ++r) {
+        // the gather: rank r > 0 sends each of its output arrays, the root receives them at
+        // their offsets (grouped point-to-point: every shard moves once over xGMI).  Within
+        // the group the first failing call is kept and the group is still closed.
+        if ((ne = ncclGroupStart()) != ncclSuccess) { result = nccl_fail(ne, "ncclGroupStart"); break; }
+        int grc = 0;
+        for (int r = 1; r < ngpu && !grc; ++r) {
             const Shard& s = sh[r];
             if (s.count == 0) continue;
-            const OutLayout L{s.count, N};
-            char* src = (char*)s.out;
-            char* dst = (char*)sh[0].out;
-            struct { size_t so, go, per; } parts[5] = {
-                {L.u0(), G.u0(), sizeof(double) * 2}, {L.traj(), G.traj(), sizeof(double) * 3 * N},
-                {L.obj(), G.obj(), sizeof(double)}, {L.status(), G.status(), sizeof(int32_t)},
-                {L.iters(), G.iters(), sizeof(int32_t)}};
-            for (const auto& p : parts) {
-                const size_t bytes = p.per * (size_t)s.count;
-                ncclSend(src + p.so, bytes, ncclChar, 0, comms[r], s.s);
-                ncclRecv(dst + p.go + p.per * (size_t)s.start, bytes, ncclChar, r, comms[0], sh[0].s);
+            mpcg_xfer x[MPCG_GATHER_ARRAYS];
+            if ((grc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) break;
+            for (const auto& p : x) {
+                if ((ne = ncclSend(s.out + p.src_offset, p.bytes, ncclChar, 0, comms[r], s.s)) != ncclSuccess) {
+                    grc = nccl_fail(ne, "ncclSend");
+                    break;
+                }
+                if ((ne = ncclRecv(sh[0].out + p.dst_offset, p.bytes, ncclChar, r, comms[0], sh[0].s)) != ncclSuccess) {
+                    grc = nccl_fail(ne, "ncclRecv");
+                    break;
+                }
             }
         }
-        if (ncclGroupEnd() != ncclSuccess) { result = -4; break; }
+        ne = ncclGroupEnd();
+        if (grc) { result = grc; break; }
+        if (ne != ncclSuccess) { result = nccl_fail(ne, "ncclGroupEnd"); break; }
         // results to the host from the root
-        hipSetDevice(sh[0].dev);
-        const char* o = (const char*)sh[0].out;
+        if ((he = hipSetDevice(sh[0].dev)) != hipSuccess) { result = hip_fail(he, "hipSetDevice"); break; }
+        const OutLayout G{B, N};
+        const char* o = sh[0].out;
         hipStream_t s0 = sh[0].s;
-        hipMemcpyAsync(u0, o + G.u0(), sizeof(double) * 2 * B, hipMemcpyDeviceToHost, s0);
-        if (traj) hipMemcpyAsync(traj, o + G.traj(), sizeof(double) * 3 * N * B, hipMemcpyDeviceToHost, s0);
-        if (obj) hipMemcpyAsync(obj, o + G.obj(), sizeof(double) * B, hipMemcpyDeviceToHost, s0);
-        if (status) hipMemcpyAsync(status, o + G.status(), sizeof(int32_t) * B, hipMemcpyDeviceToHost, s0);
-        if (iters) hipMemcpyAsync(iters, o + G.iters(), sizeof(int32_t) * B, hipMemcpyDeviceToHost, s0);
+        struct { void* host; size_t off, bytes; } back[MPCG_GATHER_ARRAYS] = {
+            {u0, G.u0(), sizeof(double) * 2 * B}, {traj, G.traj(), sizeof(double) * 3 * N * B},
+            {obj, G.obj(), sizeof(double) * B}, {status, G.status(), sizeof(int32_t) * B},
+            {iters, G.iters(), sizeof(int32_t) * B}};
+        for (const auto& b : back) {
+            if (!b.host) continue;
+            if ((he = hipMemcpyAsync(b.host, o + b.off, b.bytes, hipMemcpyDeviceToHost, s0)) != hipSuccess) {
+                result = hip_fail(he, "hipMemcpyAsync (results)");
+                break;
+            }
+        }
+        if (result) break;
         for (auto& s : sh) {
-            hipSetDevice(s.dev);
-            if (hipStreamSynchronize(s.s) != hipSuccess) result = -2;
+            if ((he = hipSetDevice(s.dev)) != hipSuccess || (he = hipStreamSynchronize(s.s)) != hipSuccess) {
+                result = hip_fail(he, "hipStreamSynchronize");
+                break;
+            }
         }
     } while (false);
     cleanup();
     return result;
 }
+
+}  // extern "C"

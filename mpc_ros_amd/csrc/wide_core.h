@@ -232,11 +232,6 @@ struct WideSolver {
     // accepted (the accepted iterate is bitwise the trial point: both are w + alpha dw)
     T c_sa = 0, c_ca = 0;
     int c_ok = 0;
-    // SPLIT: reciprocal slacks 1/(w - lo), 1/(hi - w) of the lane's four variables, from
-    // the stage data of the Newton system (same iterate) to the step statistics
-#ifdef MPCG_RD_CACHE
-    T c_rdl[4] = {0, 0, 0, 0}, c_rdu[4] = {0, 0, 0, 0};
-#endif
     static constexpr int model = MODEL;
     T lf;  // model 1: wheelbase
 
@@ -1157,10 +1152,6 @@ struct WideSolver {
                 const T hb = q < 2 ? su : (q == 2 ? (hi ? wu : su) : (hi ? au : su));
                 if (mode == 0) {
                     const T rdl = rcp(w[q] - lo), rdu = rcp(hb - w[q]);
-#ifdef MPCG_RD_CACHE
-                    c_rdl[q] = rdl;
-                    c_rdu[q] = rdu;
-#endif
                     qd = sf * hq + zl[q] * rdl + zu[q] * rdu + delta_w;
                     qv = sf * gq - mu * rdl + mu * rdu;
                 } else {
@@ -1505,11 +1496,7 @@ struct WideSolver {
         for (int q = 0; q < 4; ++q) {
             if (q < nv) {
                 const T lo = q < 2 ? sl : (q == 2 ? lo2 : lo3), up_ = q < 2 ? su : (q == 2 ? hi2 : hi3);
-#ifdef MPCG_RD_CACHE
-                const T rdl = c_rdl[q], rdu = c_rdu[q];
-#else
                 const T rdl = rcp(w[q] - lo), rdu = rcp(up_ - w[q]);
-#endif
                 const T gphi = gq[q] - mu * rdl + mu * rdu;
                 dir_var_r(w[q], zl[q], zu[q], lo, up_, gphi, dq[q], rdl, rdu, F);
             }

@@ -2,8 +2,8 @@
 
 The B problems are independent: rank r of W solves the contiguous
 slice [start, start + count) with no communication, then the per-problem results
-are gathered to rank 0 -- the only exchange on the path (RCCL over xGMI with the
-"nccl" backend; gloo on CPU in tests).  Inputs are regenerated on every rank from
+are gathered to rank 0 -- the only exchange on the path (one gather per output array,
+RCCL point-to-point over xGMI with the "nccl" backend; gloo on CPU in tests).  Inputs are regenerated on every rank from
 (seed, global index), so no input is ever sent.
 """
 from __future__ import annotations
@@ -30,28 +30,50 @@ def env_rank_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def gather_plan(total: int, world: int, row_bytes: int) -> list[dict]:
+    """Per rank: its slice and the bytes gather_rows moves for one array of `row_bytes`-byte
+    rows -- rank r > 0 sends max_shard rows (its slice, padded by at most one row) to rank 0
+    only; rank 0 sends nothing over the link."""
+    m = max_shard(total, world) if world > 0 else 0
+    out = []
+    for r in range(world):
+        start, count = shard(total, r, world)
+        out.append(dict(rank=r, start=start, count=count, send_bytes=0 if r == 0 else m * row_bytes))
+    return out
+
+
 def gather_rows(t, total: int, group=None):
     """Gather every rank's slice (rows of `t`, shard() layout) into a [total, ...] tensor on rank 0.
 
-    Shards are padded to the largest shard so that one all_gather_into_tensor moves
-    everything (RCCL all-gather: every rank sends its slice once over xGMI).  Returns
-    the assembled tensor on rank 0 and None elsewhere."""
+    One torch.distributed.gather to rank 0 (RCCL point-to-point under "nccl": each rank
+    sends only its own slice, padded to the largest shard so the messages are equal-sized;
+    no rank but 0 receives anything).  Returns the assembled tensor on rank 0 and None
+    elsewhere."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    start, count = shard(total, rank, world)
+    if t.shape[0] != count:
+        raise ValueError(f"rank {rank}: {t.shape[0]} rows, its shard holds {count}")
     m = max_shard(total, world)
-    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    pad[: t.shape[0]] = t
-    out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
+    tail = tuple(t.shape[1:])
+    if t.shape[0] == m:
+        send = t.contiguous()
+    else:
+        send = torch.zeros((m,) + tail, dtype=t.dtype, device=t.device)
+        send[:count] = t
+    root = dist.get_global_rank(group, 0) if group is not None else 0
     if rank != 0:
+        dist.gather(send, None, dst=root, group=group)
         return None
+    buf = torch.empty((world * m,) + tail, dtype=t.dtype, device=t.device)
+    dist.gather(send, list(buf.split(m, 0)), dst=root, group=group)
     parts = []
     for r in range(world):
         _, cnt = shard(total, r, world)
-        parts.append(out[r * m: r * m + cnt])
+        parts.append(buf[r * m: r * m + cnt])
     return torch.cat(parts, 0)
 
 

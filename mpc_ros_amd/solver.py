@@ -100,12 +100,13 @@ class BatchSolver:
             self._h, B, state.ctypes.data_as(dp), coeffs.ctypes.data_as(dp), u0.ctypes.data_as(dp),
             traj.ctypes.data_as(dp) if traj is not None else None, status.ctypes.data_as(ip),
             obj.ctypes.data_as(dp), iters.ctypes.data_as(ip), diag.ctypes.data_as(ip)), "mpcg_solve_ex")
-        # diag columns: restoration phases, filter entries dropped beyond its capacity, parked, 0
+        # diag columns: restoration phases, filter entries dropped beyond its capacity, parked,
+        # most filter entries held at once
         return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters, diag=diag)
 
     def solve_device(self, state, coeffs, u0, traj=None, status=None, obj=None, iters=None, stream=None, diag=None):
         """All arguments are torch tensors on this handle's GPU (float64 / int32, contiguous);
-        diag [B, 4] int32: restoration phases, filter overflows, parked, 0."""
+        diag [B, 4] int32: restoration phases, filter overflows, parked, filter peak."""
         import torch
 
         B = state.shape[0]
@@ -163,7 +164,9 @@ class BatchSolver:
 
 def solve_multi(devices, params: dict | None = None, state=None, coeffs=None, dtype: str = "fp64", **ipopt) -> dict:
     """mpcg_solve_multi: one process, the batch sharded over `devices`, results gathered to
-    devices[0] by RCCL (include/mpcg.h)."""
+    devices[0] by RCCL (include/mpcg.h).  Only ngpu = 1 has run on hardware (the GPU boxes
+    this was developed on hold one MI355X); the shard and gather arithmetic for ngpu > 1 is
+    unit-tested on the CPU (tests/test_abi.py)."""
     state = np.ascontiguousarray(state, dtype=np.float64)
     coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
     B = state.shape[0]
@@ -174,6 +177,8 @@ def solve_multi(devices, params: dict | None = None, state=None, coeffs=None, dt
     opts = dict(IPOPT_DEFAULTS)
     opts.update(ipopt)
     for k, v in opts.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"mpcg_params has no field {k!r}")
         setattr(p, k, v)
     N = p.steps
     u0 = np.zeros((B, 2))

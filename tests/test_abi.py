@@ -7,6 +7,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -143,3 +144,33 @@ def test_product_package_never_imports_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not bad.search(txt), f
+
+
+def test_multi_gpu_shard_and_gather_plan(libmpcg):
+    """mpcg_solve_multi's arithmetic through the C-ABI (no GPU): shards contiguous and
+    balanced (B % G != 0, empty shards for B < G); for each of the five output arrays the
+    messages of all GPUs tile the root's gathered buffer exactly once; rank 0's slot is in
+    place; the bytes per GPU are count x (32 + 24 N)."""
+    from mpc_ros_amd import _lib
+
+    for B, G, N in ((7, 3, 20), (2, 4, 20), (524288, 8, 20), (65537, 8, 40), (1, 1, 3), (0, 2, 20)):
+        total = libmpcg.mpcg_multi_out_bytes(B, N)
+        assert total == B * (32 + 24 * N)
+        cover = np.zeros(total, dtype=np.int32)
+        start, count = C.c_int64(), C.c_int64()
+        nxt = 0
+        for r in range(G):
+            assert libmpcg.mpcg_shard_range(B, G, r, C.byref(start), C.byref(count)) == 0
+            assert start.value == nxt and count.value == B // G + (1 if r < B % G else 0)
+            nxt += count.value
+            x = (_lib.MpcgXfer * _lib.GATHER_ARRAYS)()
+            assert libmpcg.mpcg_multi_gather_plan(B, N, G, r, x) == 0
+            assert sum(m.bytes for m in x) == count.value * (32 + 24 * N)
+            for m in x:
+                if r == 0:
+                    assert m.src_offset == m.dst_offset
+                cover[m.dst_offset:m.dst_offset + m.bytes] += 1
+        assert nxt == B
+        assert (cover == 1).all()
+    assert libmpcg.mpcg_shard_range(10, 2, 2, C.byref(start), C.byref(count)) < 0
+    assert libmpcg.mpcg_last_error()
