@@ -105,6 +105,12 @@ typedef struct mpcg_params {
      * in float -- state a tolerance a float iterate can meet (tol ~1e-5 instead of 1e-8;
      * tiny_step_tol 10 FLT_EPSILON).  Inputs and outputs stay double. */
     int32_t precision;
+    /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails; 1:
+     * stop there with RESTORATION_FAILURE (9) instead.  The fp32 solver's setting (its line
+     * search fails at a float iterate's noise floor, where the restoration phase costs a
+     * long lone-wavefront tail and rarely ends in success).  Occupies the struct's padding:
+     * sizeof(mpcg_params) is unchanged. */
+    int32_t no_restoration;
 } mpcg_params;
 
 typedef struct mpcg_handle mpcg_handle;

@@ -38,6 +38,7 @@ class MpcgParams(C.Structure):
         ("acceptable_iter", C.c_int32), ("max_soc", C.c_int32), ("watchdog_shortened_iter_trigger", C.c_int32),
         ("watchdog_trial_iter_max", C.c_int32), ("max_soft_resto_iters", C.c_int32),
         ("max_filter_resets", C.c_int32), ("filter_reset_trigger", C.c_int32), ("precision", C.c_int32),
+        ("no_restoration", C.c_int32),
     ]
 
 

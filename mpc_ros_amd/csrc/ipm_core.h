@@ -76,6 +76,7 @@ struct IpmParams {
     double compl_inf_tol;               // 1e-4
     int cpu_iter_budget;                // max_cpu_time as iterations (-1 = none): status UNKNOWN beyond
     int precision;                      // 0: fp64 (Ipopt's); 1: fp32 solver (differential drive)
+    int no_resto;                       // 1: RESTORATION_FAILURE where the restoration phase would start
 };
 
 // The Ipopt 3.12 options the reference leaves at their defaults (mpc_planner.cpp:356-368:
@@ -84,6 +85,7 @@ struct IpmParams {
 // constants (fewer wave-uniform values held through the solve); launch_wide_solve takes
 // it only when every field below equals the handle's option.
 MPCG_HD void ipopt_default_options(IpmParams& q) {
+    q.no_resto = 0;
     q.tol = 1e-8;
     q.bound_relax_factor = 1e-8;
     q.mu_init = 0.1;
@@ -125,7 +127,7 @@ inline bool ipopt_options_are_default(const IpmParams& p) {
            p.max_filter_resets == q.max_filter_resets && p.filter_reset_trigger == q.filter_reset_trigger &&
            p.tiny_step_tol == q.tiny_step_tol && p.tiny_step_y_tol == q.tiny_step_y_tol &&
            p.dual_inf_tol == q.dual_inf_tol && p.constr_viol_tol == q.constr_viol_tol &&
-           p.compl_inf_tol == q.compl_inf_tol;
+           p.compl_inf_tol == q.compl_inf_tol && p.no_resto == q.no_resto;
 }
 
 // Status numbering of CppAD::ipopt::solve_result::status_type

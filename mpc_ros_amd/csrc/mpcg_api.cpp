@@ -108,12 +108,15 @@ static void ipopt_defaults(mpcg_params* p) {
 
 // max_cpu_time as the iterations the reference's Solve affords in that time at horizon
 // N: CppAD taping 1.52 ms (N = 20) / 3.93 ms (N = 40) and derivative cost 0.225 / 0.467 ms
-// per iteration, measured in the survey, linear in N.  -1: no budget.
-// (oracle/ipm.c ora_cpu_iter_budget restates the same model for the checker.)
+// per iteration, measured in the survey, plus Ipopt's own per-iteration
+// work (KKT factorisation and solve, line search): the structured oracle's iteration on
+// one EPYC 9575F core, 0.103 ms at N = 20 (profiles/r3/cpu_iter_cost.json), taken linear
+// in N (5.14 us per stage).  0.5 s -> 1520 iterations at N = 20, 737 at N = 40.  -1: no
+// budget.  (oracle/ipm.c ora_cpu_iter_budget restates the same model for the checker.)
 static int cpu_iter_budget(double max_cpu_time, int steps) {
     if (!(max_cpu_time > 0) || max_cpu_time >= 999999.0) return -1;
     const double setup = std::fmax(0.0, 0.1205e-3 * steps - 0.89e-3);
-    const double per = std::fmax(0.0121e-3 * steps - 0.017e-3, 1e-5);
+    const double per = std::fmax(0.0121e-3 * steps - 0.017e-3, 1e-5) + 5.14e-6 * steps;
     const double b = std::floor((max_cpu_time - setup) / per);
     return b < 0 ? 0 : (b > 1e9 ? 1000000000 : (int)b);
 }
@@ -214,6 +217,7 @@ int mpcg_params_check(const mpcg_params* p) {
     if (p->model == 1 && !(p->wheelbase > 0)) return fail(-1, "model 1 needs wheelbase (LF) > 0");
     if (p->precision != 0 && p->precision != 1) return fail(-1, "precision must be 0 (fp64) or 1 (fp32)");
     if (p->precision == 1 && p->model != 0) return fail(-1, "precision 1 (fp32) runs the differential drive only");
+    if (p->no_restoration != 0 && p->no_restoration != 1) return fail(-1, "no_restoration must be 0 or 1");
     return 0;
 }
 
@@ -263,6 +267,7 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
     q.compl_inf_tol = p.compl_inf_tol;
     q.cpu_iter_budget = cpu_iter_budget(p.max_cpu_time, p.steps);
     q.precision = p.precision;
+    q.no_resto = p.no_restoration;
     return q;
 }
 

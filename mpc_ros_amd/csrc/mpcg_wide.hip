@@ -196,8 +196,10 @@ __device__ __forceinline__ int take_parked(const WideArgs& a) {
     return r;
 }
 
+// (one wavefront per SIMD: the restoration phase and the resumed solve get the whole
+// register file -- the workers are few, and the drain runs after the batch kernel)
 template <int MODEL, bool SPLIT, class T, int NB>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_resume_wide(WideArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_resume_wide(WideArgs a) {
     const int t = threadIdx.x;
     const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
@@ -318,9 +320,10 @@ int64_t wide_slots(const IpmParams& P, int64_t B) {
 }
 static size_t slot_flag_bytes(int64_t nslots) { return ((size_t)nslots * sizeof(int32_t) + 255) & ~(size_t)255; }
 // the park area: problems that enter the restoration phase (rare: ~5e-5 of the infinity set at
-// N = 20, 5e-4 at N = 40); beyond its capacity a problem ends with restoration_failure
+// N = 20, 5e-4 at N = 40, ~4e-3 with the fp32 solver at N = 40); beyond its capacity (B / 128,
+// at least 256) a problem ends with restoration_failure
 int64_t wide_park_cap(int64_t B) {
-    const int64_t c = B / 256 > 256 ? B / 256 : 256;
+    const int64_t c = B / 128 > 256 ? B / 128 : 256;
     return c < B ? c : B;
 }
 static size_t park_elems(const IpmParams& P) {
@@ -334,10 +337,11 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
            park_elems(P) * elem_bytes(P) * (size_t)pc;
 }
 
-// Resume workers (parked problems in flight at once): each holds a wavefront slot and a
-// problem's LDS for the whole batch kernel (32 workers cost the batch kernel ~7 %, 2 under
-// 1 %), and problems park rarely (~5e-5 of the infinity set at N = 20, ~5e-4 at N = 40):
-// two, and one more per 65536 problems.
+// Concurrent resume workers (parked problems in flight while the batch kernel runs): each
+// holds a wavefront slot and a problem's LDS for the whole batch kernel (32 workers cost
+// the batch kernel ~7 %, 2 under 1 %), and problems park rarely (~5e-5 of the infinity set
+// at N = 20, ~5e-4 at N = 40; ~4e-3 with the fp32 solver): two, and one more per 65536
+// problems.  What is still parked when the batch ends goes to the drain launch.
 #ifndef MPCG_RESUME_WORKERS
 #define MPCG_RESUME_WORKERS 2
 #endif
@@ -397,8 +401,15 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     }
     e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
-    const unsigned workers = (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B));
-    e = hipLaunchKernel(rf, dim3(workers), dim3(64), args, lds, fork ? aux : stream);
+    if (fork) {  // the concurrent workers
+        const unsigned workers = (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B));
+        e = hipLaunchKernel(rf, dim3(workers), dim3(64), args, lds, aux);
+        if (e != hipSuccess) return e;
+    }
+    // the drain, after the batch kernel: one worker per park entry, so the problems still
+    // parked when the batch ends run side by side (a worker finding nothing left exits at
+    // once) -- the tail is the longest restoration, not their sum over a few workers
+    e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
     if (fork) {
         e = hipEventRecord(ev_join, aux);

@@ -23,7 +23,7 @@ IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor
 # stalls): acceptable termination at 1e-3 and a 300-iteration cap end such stalls (measured
 # on the infinity set: the controls of those problems equal the fp64 solution to ~1e-5).
 FP32_OPTIONS = dict(precision=1, tol=2e-4, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
-                    acceptable_tol=1e-3, max_iter=300)
+                    acceptable_tol=1e-3, max_iter=300, no_restoration=1)
 
 
 class BatchSolver:

@@ -90,7 +90,10 @@ void ora_ipm_default_opts(ora_ipm_opts* o) {
 int ora_cpu_iter_budget(double max_cpu_time, int steps) {
     if (!(max_cpu_time > 0) || max_cpu_time >= 999999.0) return -1;  /* Ipopt: no limit at >= 1e6 */
     const double setup = fmax(0.0, 0.1205e-3 * steps - 0.89e-3);     /* 1.52 ms @20, 3.93 ms @40 */
-    const double per = fmax(0.0121e-3 * steps - 0.017e-3, 1e-5);      /* 0.225 ms @20, 0.467 ms @40 */
+    /* per iteration: CppAD's derivatives (0.225 ms @20, 0.467 ms @40) + Ipopt's own work,
+     * calibrated by this oracle's structured-KKT iteration on one EPYC 9575F core (0.103 ms
+     * @20, linear in N: 5.14 us per stage; profiles/r3/cpu_iter_cost.json) */
+    const double per = fmax(0.0121e-3 * steps - 0.017e-3, 1e-5) + 5.14e-6 * steps;
     const double b = floor((max_cpu_time - setup) / per);
     return b < 0 ? 0 : (b > 1e9 ? 1000000000 : (int)b);
 }

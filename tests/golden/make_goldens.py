@@ -184,14 +184,14 @@ def ipopt_features():
             out[f"{name}__{k}"] = v
         print(name, "status", d["status"].tolist(), "iters", d["iters"].tolist())
         print("   diag (soc, watchdog, soft, resto, resto iters):", d["diag"].tolist())
-    # the max_cpu_time budget forced low: 0.004 s -> ora_cpu_iter_budget iterations at N = 20
+    # the max_cpu_time budget forced low: 0.005 s -> ora_cpu_iter_budget iterations at N = 20
     P = PLUGIN
     st, cf = infinity.make_problems(np.arange(0, 32))
-    budget = O.cpu_iter_budget(0.004, 20)
+    budget = O.cpu_iter_budget(0.005, 20)
     d = solve_set(P, st, cf, opts=O.ref_opts(20, cpu_iter_budget=budget))
     for k, v in d.items():
         out[f"budget__{k}"] = v
-    out["budget__max_cpu_time"] = np.float64(0.004)
+    out["budget__max_cpu_time"] = np.float64(0.005)
     out["budget__iter_budget"] = np.int32(budget)
     print("budget", budget, "status", np.unique(d["status"], return_counts=True))
     out["keys"] = np.array(params.KEYS)

@@ -127,7 +127,7 @@ def test_filter_beyond_lds_matches_oracle(torch_cuda, features_golden):
 
 
 def test_cpu_time_budget_matches_oracle(torch_cuda, features_golden):
-    """max_cpu_time forced low (0.004 s -> its iteration budget at N = 20): problems that
+    """max_cpu_time forced low (0.005 s -> its iteration budget at N = 20): problems that
     need more iterations stop with status 14 (unknown, Ipopt's CPUTIME_EXCEEDED) at the
     budget, with the oracle's last iterate."""
     g = features_golden["budget"]

@@ -100,7 +100,7 @@ int main(int argc, char** argv) {
     P.max_soc = 4; P.kappa_soc = 0.99; P.watchdog_trigger = 10; P.watchdog_trial_max = 3;
     P.soft_resto_factor = 0.9999; P.max_soft_resto_iters = 10; P.obj_max_inc = 5; P.max_filter_resets = 5;
     P.filter_reset_trigger = 5; P.tiny_step_tol = 10 * 2.220446049250313e-16; P.tiny_step_y_tol = 1e-2;
-    P.dual_inf_tol = 1; P.constr_viol_tol = 1e-4; P.compl_inf_tol = 1e-4; P.cpu_iter_budget = 2215; P.precision = 0;
+    P.dual_inf_tol = 1; P.constr_viol_tol = 1e-4; P.compl_inf_tol = 1e-4; P.cpu_iter_budget = 1520; P.precision = 0;
     double *dst, *dcf;
     unsigned long long* dacc;
     int *dit, *dss;
