@@ -25,9 +25,10 @@ struct WideArgs {
     double* obj;
     int32_t* iters;
     int32_t* diag;         // [B][4] restoration phases, filter overflows, parked, 0 (or null)
-    void* slots;           // nslots workspaces of WideLayout::spill() elements of T (the rare paths' copies)
+    void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
     int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
-    int32_t nslots;
+    int32_t nslots;        // kXcds partitions of nslots / kXcds slots, one per XCD
+    int32_t slot_elems;    // WideLayout::spill() rounded up to whole 128-byte lines
     // parked problems (the restoration phase, continued by k_resume_wide while the batch
     // kernel runs): count, capacity, problem index, ready flag and state of each; the entries
     // taken by the resume workers; the batch kernel's finished workgroups
@@ -38,33 +39,50 @@ struct WideArgs {
     int32_t* park_taken;
     int32_t* done;
     void* park;
+    int64_t park_stride;   // elements of T per park entry (WideSolver::park_elems, whole 128-byte lines)
 };
-// the wavefront's end in k_solve_wide (after its results / its parked state are written)
+// the wavefront's end in k_solve_wide (after its results / its parked state are written).
+// No fence: the count only tells the resume workers when every workgroup has finished, and
+// a parking workgroup has released its entry (agent scope) before it counts itself.
 __device__ __forceinline__ void block_done(int32_t* done) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_wave_barrier();
     if (threadIdx.x == 0) atomicAdd(done, 1);
 }
 
-// A workspace slot for the wavefront's problem: the first free one from blockIdx mod
-// nslots on (nslots >= the resident wavefronts, so the first probe normally succeeds;
-// with fewer, a wavefront waits for a resident one to finish and release its slot).
-// Vector atomics through the L2 (device scope).
+// The XCD the wavefront runs on (HW_REG_XCC_ID, 0..7 on MI355X).
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 15) % kXcds;
+}
+
+// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on:
+// the first free one from blockIdx on (a partition holds 4x the wavefronts an XCD keeps
+// resident, so the first probe normally succeeds; with fewer, a wavefront waits for a
+// resident one on its XCD to finish and release its slot).  A slot is therefore only ever
+// touched through one XCD's L2, and every owner writes a slot location before it reads it
+// (the watchdog, acceptable-point, SOC and soft-restoration copies, the filter's workspace
+// entries): no data crosses wavefronts, so claim and release need no acquire / release
+// fence (an agent-scope release is a write-back of the whole XCD L2, buffer_wbl2, per
+// wavefront: 1.6 GB of write traffic per B = 65,536 launch when it was there).  Slot
+// lines are whole 128-byte lines, so two XCDs never share one.  Vector atomics (device
+// scope) on the flags.
 __device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int64_t hint) {
-    int s = (int)(hint % nslots);
+    const int per = nslots / kXcds, base = xcc_id() * per;
+    int s = (int)(hint % per);
     int r = 0;
     if (threadIdx.x == 0) {
         for (;;) {
-            if (atomicCAS(&flags[s], 0, 1) == 0) break;
-            s = s + 1 == nslots ? 0 : s + 1;
-            if (s == (int)(hint % nslots)) __builtin_amdgcn_s_sleep(8);
+            if (atomicCAS(&flags[base + s], 0, 1) == 0) break;
+            s = s + 1 == per ? 0 : s + 1;
+            if (s == (int)(hint % per)) __builtin_amdgcn_s_sleep(8);
         }
-        r = s;
+        r = base + s;
     }
     return __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
 }
 __device__ __forceinline__ void release_slot(int32_t* flags, int s) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the slot's last stores before its release
     __builtin_amdgcn_wave_barrier();
     if (threadIdx.x == 0) atomicExch(&flags[s], 0);
 }
@@ -80,8 +98,10 @@ __device__ __forceinline__ void release_slot(int32_t* flags, int s) {
 template <class Solver>
 __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked);
 
-template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_solve_wide(WideArgs a) {
+// WPE: wavefronts per SIMD the register allocation is for -- 2 (256 VGPRs), or 1 (512) for
+// the instances whose LDS per problem allows at most 4 problems per CU anyway (wide_kernel)
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
     const int t = threadIdx.x;
@@ -94,10 +114,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     wv.t = t;
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
-    const WideLayout Lw(Pk.N, Pk.filter_cap, MODEL);
     const int slot = claim_slot(a.slot_flags, a.nslots, (int64_t)blockIdx.x);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
-    Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * Lw.spill());
+    Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     S.solve();
     if (S.status == Solver::NEED_RESTO) {
         // the restoration phase runs in k_resume_wide: park the problem
@@ -105,7 +124,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (t == 0) e = atomicAdd(a.park_count, 1);
         e = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
         if (e < a.park_cap) {
-            S.park((T*)a.park + (int64_t)e * Solver::park_elems(Lw));
+            S.park((T*)a.park + (int64_t)e * a.park_stride);
             if (t == 0) a.park_idx[e] = p;
             // the entry is complete: its ready flag after the stores (release, device scope)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -214,7 +233,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
         DevWave wv;
         wv.t = t;
-        T* ent = (T*)a.park + (int64_t)e * Solver::park_elems(Lw);
+        T* ent = (T*)a.park + (int64_t)e * a.park_stride;
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
         S.unpark(ent);
         S.finish_resto();
@@ -282,8 +301,14 @@ static const void* resume_kernel(const IpmParams& P) {
          : split ? (const void*)k_resume_wide<0, true, double, 1> : (const void*)k_resume_wide<0, false, double, 1>;
 }
 
-// (model, split, precision, blocks, default options) -> kernel instance; null if none
-static const void* wide_kernel(const IpmParams& P) {
+// (model, split, precision, blocks, default options, waves per SIMD) -> kernel instance;
+// null if none.  An fp64 problem of more than 32 KB of LDS (N >= 35; every N > 64) leaves
+// room for at most 4 problems per CU (160 KB), one wavefront per SIMD: its instance is
+// register-allocated for one (512 VGPRs, no spills) instead of two.
+// A batch the device holds at one wavefront per SIMD (B <= kLoneBatch: 4 x 256 CUs) runs
+// the benchmark configuration's instance allocated for one wavefront per SIMD as well.
+constexpr int64_t kLoneBatch = 1024;
+static const void* wide_kernel(const IpmParams& P, int64_t B) {
     const bool split = P.N <= 32;
     const bool f32 = P.precision == 1;
     const int nb = P.N > 64 ? 2 : 1;
@@ -292,23 +317,30 @@ static const void* wide_kernel(const IpmParams& P) {
     if (f32)
         return nb == 2 ? (const void*)k_solve_wide<0, false, float, 2>
              : split ? (const void*)k_solve_wide<0, true, float, 1> : (const void*)k_solve_wide<0, false, float, 1>;
+    const bool one = wide_lds_bytes(P) > 32768;
     if (P.model == 1)
-        return nb == 2 ? (const void*)k_solve_wide<1, false, double, 2>
-             : split ? (const void*)k_solve_wide<1, true, double, 1> : (const void*)k_solve_wide<1, false, double, 1>;
+        return nb == 2 ? (const void*)k_solve_wide<1, false, double, 2, false, 1>
+             : split ? (const void*)k_solve_wide<1, true, double, 1>
+             : one   ? (const void*)k_solve_wide<1, false, double, 1, false, 1>
+                     : (const void*)k_solve_wide<1, false, double, 1>;
     if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
-        return (const void*)k_solve_wide<0, true, double, 1, true>;
-    return nb == 2 ? (const void*)k_solve_wide<0, false, double, 2>
-         : split ? (const void*)k_solve_wide<0, true, double, 1> : (const void*)k_solve_wide<0, false, double, 1>;
+        return B <= kLoneBatch ? (const void*)k_solve_wide<0, true, double, 1, true, 1>
+                               : (const void*)k_solve_wide<0, true, double, 1, true>;
+    return nb == 2 ? (const void*)k_solve_wide<0, false, double, 2, false, 1>
+         : split ? (const void*)k_solve_wide<0, true, double, 1>
+         : one   ? (const void*)k_solve_wide<0, false, double, 1, false, 1>
+                 : (const void*)k_solve_wide<0, false, double, 1>;
 }
 
 // Workspace slots for a batch of B: four times the wavefronts the device can hold resident at
-// once (occupancy of the instance at its LDS size times the CUs), at most B.  A wavefront
-// claims slot blockIdx mod nslots, or the next free one: with the margin, a slow problem
-// still holding a slot rarely makes a later wavefront probe further.
+// once (occupancy of the instance at its LDS size times the CUs), at most B (at least 32 per
+// XCD), in kXcds equal partitions.  A wavefront claims slot blockIdx mod the partition size
+// in its XCD's partition, or the next free one: with the margin, a slow problem still
+// holding a slot rarely makes a later wavefront probe further.
 int64_t wide_slots(const IpmParams& P, int64_t B) {
     if (B <= 0) return 0;
     int64_t n = 4096;  // (fallback if the runtime cannot say)
-    const void* fn = wide_kernel(P);
+    const void* fn = wide_kernel(P, B);
     int dev = 0, cus = 0, per = 0;
     if (fn && hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
@@ -316,7 +348,17 @@ int64_t wide_slots(const IpmParams& P, int64_t B) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64, wide_lds_bytes(P)) == hipSuccess && per > 0 &&
         cus > 0)
         n = 4 * (int64_t)per * cus;
-    return n < B ? n : B;
+    n = n < B ? n : B;
+    int64_t part = (n + kXcds - 1) / kXcds;
+    const int64_t floor_ = B < 32 ? B : 32;
+    part = part > floor_ ? part : floor_;
+    return part * kXcds;
+}
+// a slot's elements: WideLayout::spill() rounded up to whole 128-byte lines
+static int64_t slot_elems(const IpmParams& P) {
+    const int64_t e = P.precision == 1 ? 4 : 8, per_line = 128 / e;
+    const int64_t n = WideLayout(P.N, P.filter_cap, P.model).spill();
+    return (n + per_line - 1) / per_line * per_line;
 }
 static size_t slot_flag_bytes(int64_t nslots) { return ((size_t)nslots * sizeof(int32_t) + 255) & ~(size_t)255; }
 // the park area: problems that enter the restoration phase (rare: ~5e-5 of the infinity set at
@@ -328,12 +370,13 @@ int64_t wide_park_cap(int64_t B) {
 }
 static size_t park_elems(const IpmParams& P) {
     const WideLayout L(P.N, P.filter_cap, P.model);
-    return (size_t)(32 + L.total() + L.slot());  // (WideSolver::park_elems)
+    const size_t n = (size_t)(32 + L.total() + L.slot()), per_line = 128 / elem_bytes(P);  // (WideSolver::park_elems)
+    return (n + per_line - 1) / per_line * per_line;
 }
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
     return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) + slot_flag_bytes(pc) +
-           (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns +
+           (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns +
            park_elems(P) * elem_bytes(P) * (size_t)pc;
 }
 
@@ -354,7 +397,7 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
-    const void* fn = wide_kernel(P);
+    const void* fn = wide_kernel(P, B);
     if (!fn) return hipErrorInvalidValue;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
@@ -377,13 +420,14 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     int32_t* pready = (int32_t*)w;
     w += slot_flag_bytes(pc);
     void* slots = w;
-    w += (size_t)WideLayout(P.N, P.filter_cap, P.model).spill() * elem_bytes(P) * (size_t)ns;
+    w += (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns;
     void* park = w;
     e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, park counters)
     if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
     if (e != hipSuccess) return e;
-    const WideArgs a{P, B, order, state, coeffs, u0, traj, status, obj, iters, diag, slots, flags, (int32_t)ns,
-                     pcount, (int32_t)pc, pidx, pready, pcount + 1, pcount + 2, park};
+    const WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
+                     (int32_t)ns, (int32_t)slot_elems(P), pcount, (int32_t)pc, pidx, pready, pcount + 1, pcount + 2,
+                     park, (int64_t)park_elems(P)};
     void* args[] = {(void*)&a};
     const void* rf = resume_kernel(P);
     e = hipFuncGetAttributes(&fa, rf);
