@@ -3672,7 +3672,7 @@ struct WideSolver {
                 }
                 return IPM_RESTORATION_FAILURE;
             }
-            if (P.no_resto) return IPM_RESTORATION_FAILURE;  // (mpcg_params no_restoration)
+            if (P.no_resto) return IPM_RESTORATION_FAILURE;  // (mpcg_params no_restoration; oracle restoration = 0)
             in_soft = 0;
             soft_count = 0;
             wd_short = 0;

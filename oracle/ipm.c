@@ -1041,7 +1041,7 @@ static int find_trial_point(ipm* S, int goto_resto) {
         }
         if (!accept) {
             if (!S->in_soft) augment_filter(S);
-            if (S->is_resto || !o->restoration || S->m == 0) return ORA_RESTORATION_FAILURE;
+            if (S->is_resto || S->m == 0) return ORA_RESTORATION_FAILURE;
             /* almost feasible: restore the stored acceptable point, if any */
             if (S->theta <= 1e-2 * o->tol) {
                 if (S->have_acc) {
@@ -1050,6 +1050,9 @@ static int find_trial_point(ipm* S, int goto_resto) {
                 }
                 return ORA_RESTORATION_FAILURE;
             }
+            /* (restoration = 0: stop where the restoration phase would start -- the
+             * device's no_restoration option) */
+            if (!o->restoration) return ORA_RESTORATION_FAILURE;
             if (((orig_ctx*)S->P->ctx)->mI > 0) return ORA_RESTORATION_FAILURE;
             S->in_soft = 0;
             S->soft_count = 0;

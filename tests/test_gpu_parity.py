@@ -198,9 +198,10 @@ def test_empty_batch(torch_cuda):
 
 
 def test_full_size_properties(torch_cuda, oracle):
-    """B = 65536 (the benchmark shard): every problem solves; results are deterministic
-    and independent of batch position; a random sample agrees with the oracle and
-    carries a first-order certificate."""
+    """B = 65536 (the benchmark shard): every problem solves (status 1, the two that enter
+    the restoration phase included); results are deterministic and independent of batch
+    position; a random sample and every parked (restoration) problem agree with the
+    oracle, restoration counts included; no filter entry is dropped."""
     torch = torch_cuda
     from mpc_ros_amd import infinity, params
 
@@ -215,22 +216,66 @@ def test_full_size_properties(torch_cuda, oracle):
         u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
         traj = torch.empty((B, 3, 20), dtype=torch.float64, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)
-        s.solve_device(tst, tcf, u0, traj, status)
+        diag = torch.empty((B, 4), dtype=torch.int32, device=dev)
+        s.solve_device(tst, tcf, u0, traj, status, diag=diag)
         torch.cuda.synchronize()
-        outs.append((u0.cpu().numpy(), traj.cpu().numpy(), status.cpu().numpy()))
+        outs.append((u0.cpu().numpy(), traj.cpu().numpy(), status.cpu().numpy(), diag.cpu().numpy()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])  # deterministic
-    u0, traj, status = outs[0]
+    np.testing.assert_array_equal(outs[0][3], outs[1][3])
+    u0, traj, status, dg = outs[0]
     assert np.isfinite(u0).all() and np.isfinite(traj).all()
-    assert np.mean(status == 1) > 0.99
+    assert (status == 1).all()
+    assert (dg[:, 1] == 0).all()  # no filter entry dropped
+    parked = np.flatnonzero(dg[:, 2] == 1)
+    assert len(parked) >= 1 and (dg[parked, 0] >= 1).all() and (dg[dg[:, 2] == 0, 0] == 0).all()
     rng = np.random.default_rng(11)
-    sample = np.sort(rng.choice(B, 48, replace=False))
+    sample = np.union1d(np.sort(rng.choice(B, 48, replace=False)), parked)
     alone = s.solve(st[sample], cf[sample])
     np.testing.assert_array_equal(alone["u0"], u0[sample])  # batch-position invariance
     ref = oracle_ref(oracle, P, st[sample], cf[sample])
     np.testing.assert_array_equal(ref["status"], status[sample])
+    np.testing.assert_array_equal(ref["diag"][:, 3], dg[sample, 0])
     np.testing.assert_allclose(u0[sample], ref["u0"], atol=ATOL)
     # controls inside the box (honor_original_bounds)
     assert np.abs(u0[:, 0]).max() <= P["ANGVEL"] and np.abs(u0[:, 1]).max() <= P["MAXTHR"]
+
+
+def test_full_size_N40_restoration(torch_cuda, oracle):
+    """B = 65536 at N = 40 (the 512-VGPR instance): every problem ends with status 1; every
+    problem that went through the restoration phase (32) matches the oracle."""
+    from mpc_ros_amd import infinity, params
+
+    B = 65536
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=40)
+    st, cf = infinity.make_problems(np.arange(B))
+    r = solver_for(P).solve(st, cf)
+    assert (r["status"] == 1).all() and (r["diag"][:, 1] == 0).all()
+    parked = np.flatnonzero(r["diag"][:, 2] == 1)
+    assert len(parked) >= 10
+    ref = oracle_ref(oracle, P, st[parked], cf[parked])
+    sub = {k: r[k][parked] for k in ("u0", "traj", "status", "obj", "iters", "diag")}
+    check_against(sub, ref, min_same_iters=1.0)
+
+
+def test_no_restoration_option_matches_oracle(torch_cuda, features_golden, oracle):
+    """mpcg_params.no_restoration = 1 (the fp32 solver's setting) against the oracle with its
+    restoration phase off: status 9 (or the acceptable point) where Ipopt would enter it,
+    the same last iterate."""
+    for name in ("resto_N20", "resto_N40"):
+        g = features_golden[name]
+        N = int(g["P"]["STEPS"])
+        ref = oracle.mpc_solve_batch(g["P"], g["state"], g["coeffs"], opts=oracle.ref_opts(N, restoration=0),
+                                     nthreads=8, diag=True)
+        r = solver_for(g["P"], no_restoration=1).solve(g["state"], g["coeffs"])
+        assert (r["diag"][:, 0] == 0).all() and (r["diag"][:, 2] == 0).all()
+        assert (ref["status"] != 1).any()
+        np.testing.assert_array_equal(r["status"], ref["status"])
+        np.testing.assert_array_equal(r["iters"], ref["iters"])
+        np.testing.assert_allclose(r["u0"], ref["u0"], rtol=0, atol=ATOL)
+        np.testing.assert_allclose(r["traj"], ref["traj"], rtol=0, atol=ATOL)
+        # (a stopped iterate: resto_N40's 19304 stops after 99 iterations at an objective of
+        # 2e8, where the two agree to 7e-8 relative)
+        np.testing.assert_allclose(r["obj"], ref["obj"], rtol=1e-6)
 
 
 def test_bicycle_matches_oracle(torch_cuda, bicycle_golden):
