@@ -12,9 +12,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmpcg.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_track.hip", "mpcg_api.cpp", "mpcg_multi.cpp",
-                                           "mpc_planner.cpp")]
-HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_wide_inst.hip", "mpcg_track.hip", "mpcg_api.cpp",
+                                           "mpcg_multi.cpp", "mpc_planner.cpp")]
+INST = os.path.join(CSRC, "mpcg_wide_inst.hip")
+N_INST = 10  # MPCG_INST groups of mpcg_wide_inst.hip (mpcg_wide_kern.h)
+HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h",
+                                           "mpcg_wide_kern.h")] + [
     os.path.join(ROOT, "include", f) for f in ("mpcg.h", "mpc_planner.h")]
 ARCH = os.environ.get("MPCG_OFFLOAD_ARCH", "gfx950")
 
@@ -53,24 +56,55 @@ def stale() -> bool:
     return built_id() != source_hash()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def compile_units() -> list:
+    """(source, extra flags, object name) of every translation unit: the kernel instance
+    groups of mpcg_wide_inst.hip (the bulk of the compile time) and the other sources."""
+    units = [(INST, [f"-DMPCG_INST={g}"], f"inst{g}.o") for g in range(N_INST)]
+    units += [(s, [], os.path.basename(s) + ".o") for s in SOURCES if s != INST]
+    return units
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
     if not force and not stale():
         return LIB
     # (-disable-promote-alloca-to-lds: the solver owns the whole dynamic LDS from address 0;
     # the backend would otherwise move a private array into static LDS, which the launch
     # refuses -- mpcg_wide.hip checks sharedSizeBytes == 0)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mllvm", "-disable-promote-alloca-to-lds",
-           "-Wno-unused-result", "-Wno-unused-value",
-           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"']
-    cmd.append("-Rpass-analysis=kernel-resource-usage")
-    cmd += SOURCES + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-mllvm", "-disable-promote-alloca-to-lds",
+             "-Wno-unused-result", "-Wno-unused-value",
+             f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"',
+             "-Rpass-analysis=kernel-resource-usage"]
+    tmp = tempfile.mkdtemp(prefix="mpcg_build_")
+    try:
+        def cc(unit):
+            src, extra, obj = unit
+            cmd = [hipcc(), "-c"] + flags + extra + [src, "-o", os.path.join(tmp, obj)]
+            return cmd, subprocess.run(cmd, capture_output=True, text=True)
+
+        units = compile_units()
+        jobs = jobs or min(len(units), max(1, min(os.cpu_count() or 1, 16)))
+        with ThreadPoolExecutor(jobs) as ex:
+            results = list(ex.map(cc, units))
+        remarks = ""
+        for cmd, r in results:
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            remarks += r.stderr
+        link = [hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared"] + [os.path.join(tmp, u[2]) for u in units] + [
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
     if verbose:
-        sys.stderr.write(r.stderr)
-    usage = kernel_resources(r.stderr)
+        sys.stderr.write(remarks)
+    usage = kernel_resources(remarks)
     bad = [k for k, u in usage.items() if ("k_solve_wide" in k or "k_resume_wide" in k) and u.get("LDS Size [bytes/block]", 0) != 0]
     if bad:
         os.remove(LIB + ".tmp")

@@ -1,0 +1,290 @@
+// mpc_ros_amd/csrc/mpcg_wide_kern.h -- the solver kernels of mpcg_wide.hip (one problem per
+// wavefront, wide_core.h) as templates.  Each instance is compiled in its own translation
+// unit (mpcg_wide_inst.hip, one group per MPCG_INST value, built in parallel); the
+// dispatcher in mpcg_wide.hip reaches them through solve_kernel_fn / resume_kernel_fn.
+//
+// One workgroup = one wavefront = one problem; the problem's whole state lives in
+// the workgroup's LDS (WideLayout: 19.9 KB at N = 20, i.e. 8 problems resident per
+// CU).  Workgroups are dispatched by the hardware as CUs free up, so a slow problem
+// occupies one wavefront slot while the rest of the batch streams past it.
+#ifndef MPCG_WIDE_KERN_H
+#define MPCG_WIDE_KERN_H
+#include <hip/hip_runtime.h>
+
+#include "mpcg_internal.h"
+#include "wave_dev.h"
+#include "wide_core.h"
+
+namespace mpcg {
+
+
+struct WideArgs {
+    IpmParams P;
+    int64_t B;
+    const int32_t* order;  // workgroup -> problem (NULL: identity)
+    const double* state;
+    const double* coeffs;
+    double* u0;
+    double* traj;
+    int32_t* status;
+    double* obj;
+    int32_t* iters;
+    int32_t* diag;         // [B][4] restoration phases, filter overflows, parked, 0 (or null)
+    void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
+    int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
+    int32_t nslots;        // kXcds partitions of nslots / kXcds slots, one per XCD
+    int32_t slot_elems;    // WideLayout::spill() rounded up to whole 128-byte lines
+    // parked problems (the restoration phase, continued by k_resume_wide while the batch
+    // kernel runs): count, capacity, problem index, ready flag and state of each; the entries
+    // taken by the resume workers; the batch kernel's finished workgroups
+    int32_t* park_count;
+    int32_t park_cap;
+    int64_t* park_idx;
+    int32_t* park_ready;
+    int32_t* park_taken;
+    int32_t* done;
+    void* park;
+    int64_t park_stride;   // elements of T per park entry (WideSolver::park_elems, whole 128-byte lines)
+};
+// the wavefront's end in k_solve_wide (after its results / its parked state are written).
+// No fence: the count only tells the resume workers when every workgroup has finished, and
+// a parking workgroup has released its entry (agent scope) before it counts itself.
+__device__ __forceinline__ void block_done(int32_t* done) {
+    __builtin_amdgcn_wave_barrier();
+    if (threadIdx.x == 0) atomicAdd(done, 1);
+}
+
+// The XCD the wavefront runs on (HW_REG_XCC_ID, 0..7 on MI355X).
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 15) % kXcds;
+}
+
+// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on:
+// the first free one from blockIdx on (a partition holds 4x the wavefronts an XCD keeps
+// resident, so the first probe normally succeeds; with fewer, a wavefront waits for a
+// resident one on its XCD to finish and release its slot).  A slot is therefore only ever
+// touched through one XCD's L2, and every owner writes a slot location before it reads it
+// (the watchdog, acceptable-point, SOC and soft-restoration copies, the filter's workspace
+// entries): no data crosses wavefronts, so claim and release need no acquire / release
+// fence (an agent-scope release is a write-back of the whole XCD L2, buffer_wbl2, per
+// wavefront: 1.6 GB of write traffic per B = 65,536 launch when it was there).  Slot
+// lines are whole 128-byte lines, so two XCDs never share one.  Vector atomics (device
+// scope) on the flags.
+__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int64_t hint) {
+    const int per = nslots / kXcds, base = xcc_id() * per;
+    int s = (int)(hint % per);
+    int r = 0;
+    if (threadIdx.x == 0) {
+        for (;;) {
+            if (atomicCAS(&flags[base + s], 0, 1) == 0) break;
+            s = s + 1 == per ? 0 : s + 1;
+            if (s == (int)(hint % per)) __builtin_amdgcn_s_sleep(8);
+        }
+        r = base + s;
+    }
+    return __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+}
+__device__ __forceinline__ void release_slot(int32_t* flags, int s) {
+    __builtin_amdgcn_wave_barrier();
+    if (threadIdx.x == 0) atomicExch(&flags[s], 0);
+}
+
+// 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
+// budget of 256 per lane lets all of them be resident
+// SPLIT (N <= 32): the recursions and the step statistics use both half-waves (wide_core.h)
+// T: the solver's arithmetic type (double; float for precision 1).  Inputs and outputs
+// stay double at the boundary.
+// NB: stage blocks (2 for 64 < N <= 128, lane t owning stages t and 64 + t).
+// DEFOPT: the Ipopt options are the reference's defaults (ipopt_default_options), compiled
+// as constants.
+template <class Solver>
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked);
+
+// WPE: wavefronts per SIMD the register allocation is for -- 2 (256 VGPRs), or 1 (512) for
+// the instances whose LDS per problem allows at most 4 problems per CU anyway (wide_kernel)
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_solve_wide(WideArgs a) {
+    if ((int64_t)blockIdx.x >= a.B) return;
+    const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
+    const int t = threadIdx.x;
+    IpmProblem<T> pr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
+    DevWave wv;
+    wv.t = t;
+    IpmParams Pk = a.P;
+    if constexpr (DEFOPT) ipopt_default_options(Pk);
+    const int slot = claim_slot(a.slot_flags, a.nslots, (int64_t)blockIdx.x);
+    typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
+    Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
+    S.solve();
+    if (S.status == Solver::NEED_RESTO) {
+        // the restoration phase runs in k_resume_wide: park the problem
+        int e = 0;
+        if (t == 0) e = atomicAdd(a.park_count, 1);
+        e = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
+        if (e < a.park_cap) {
+            S.park((T*)a.park + (int64_t)e * a.park_stride);
+            if (t == 0) a.park_idx[e] = p;
+            // the entry is complete: its ready flag after the stores (release, device scope)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_wave_barrier();
+            if (t == 0) atomicExch(&a.park_ready[e], 1);
+            release_slot(a.slot_flags, slot);
+            block_done(a.done);
+            return;
+        }
+        S.status = IPM_RESTORATION_FAILURE;  // (more parked problems than the park area holds)
+    }
+    write_out(a, S, p, 0);
+    release_slot(a.slot_flags, slot);
+    block_done(a.done);
+}
+
+// results of problem p (u0, status, iterations, objective, trajectory; honor_original_bounds)
+template <class Solver>
+__device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked) {
+    const int t = threadIdx.x;
+    if (a.diag && t == 0) {
+        a.diag[p * 4 + 0] = S.n_resto;
+        a.diag[p * 4 + 1] = S.n_fover;
+        a.diag[p * 4 + 2] = parked;
+        a.diag[p * 4 + 3] = S.nf_peak;
+    }
+    const double o = (double)S.objective_out();
+    const int N = a.P.N;
+    if (t == 0) {
+        a.u0[p * 2 + 0] = (double)S.x_ctrl(0, 0);
+        a.u0[p * 2 + 1] = (double)S.x_ctrl(1, 0);
+        if (a.status) a.status[p] = S.status;
+        if (a.iters) a.iters[p] = S.iter;
+        if (a.obj) a.obj[p] = o;
+    }
+    if (a.traj) {
+        double* tr = a.traj + p * 3 * N;
+        for (int k = t; k < N; k += 64) {
+            tr[k] = (double)S.x_state(0, k);
+            tr[N + k] = (double)S.x_state(1, k);
+            tr[2 * N + k] = (double)S.x_state(2, k);
+        }
+    }
+}
+
+// The parked problems: the restoration phase (WideSolver<..., RESTO> out of line) and the
+// rest of the solve, from the state k_solve_wide parked -- the same solver instance, so the
+// iterates are those the first kernel would have continued with.  A separate kernel keeps
+// the call out of the batch kernel's register allocation.  It runs on a second stream
+// alongside the batch kernel: a few workers take parked problems as they appear (a problem
+// that parks early in the batch is resumed while the batch still runs) and exit once every
+// workgroup of the batch kernel has finished and every parked problem is taken.  A worker
+// that sees no progress of the batch kernel for 20 s exits (the batch kernel failed).
+__device__ __forceinline__ int take_parked(const WideArgs& a) {
+    int r = -1;
+    if (threadIdx.x == 0) {
+        uint64_t t0 = wall_clock64();
+        int last_done = -1;
+        for (;;) {
+            const int d = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            int c = __hip_atomic_load(a.park_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            c = c < a.park_cap ? c : a.park_cap;
+            const int tk = __hip_atomic_load(a.park_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk < c) {
+                if (atomicCAS(a.park_taken, tk, tk + 1) == tk) {
+                    r = tk;
+                    break;
+                }
+                continue;
+            }
+            // (a workgroup parks before it counts itself done: all parked once done == B)
+            if ((int64_t)d >= a.B && tk >= c) break;
+            if (d != last_done) {
+                last_done = d;
+                t0 = wall_clock64();
+            } else if (wall_clock64() - t0 > (uint64_t)2000000000) {  // 20 s at 100 MHz
+                break;
+            }
+            __builtin_amdgcn_s_sleep(32);
+        }
+        if (r >= 0) {  // the entry's stores are visible once its ready flag is
+            while (__hip_atomic_load(&a.park_ready[r], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    r = __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return r;
+}
+
+// (one wavefront per SIMD: the restoration phase and the resumed solve get the whole
+// register file -- the workers are few, and the drain runs after the batch kernel)
+template <int MODEL, bool SPLIT, class T, int NB>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_resume_wide(WideArgs a) {
+    const int t = threadIdx.x;
+    const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
+    typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
+    for (;;) {
+        const int e = take_parked(a);
+        if (e < 0) return;
+        const int64_t p = a.park_idx[e];
+        IpmProblem<T> pr;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
+        DevWave wv;
+        wv.t = t;
+        T* ent = (T*)a.park + (int64_t)e * a.park_stride;
+        Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
+        S.unpark(ent);
+        S.finish_resto();
+        write_out(a, S, p, 1);
+    }
+}
+
+// Kernel instances (host stubs), defined in mpcg_wide_inst.hip: the instance of
+// k_solve_wide<MODEL, SPLIT, T, NB, DEFOPT, WPE> / k_resume_wide<MODEL, SPLIT, T, NB>.
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT, int WPE>
+const void* solve_kernel_fn();
+template <int MODEL, bool SPLIT, class T, int NB>
+const void* resume_kernel_fn();
+
+// (group, model, split, type, blocks, default options, waves per SIMD): the instances the
+// library carries; group = the MPCG_INST translation unit that compiles it
+#define MPCG_WIDE_SOLVE_INSTANCES(X)          \
+    X(0, 0, true, double, 1, true, 2)         \
+    X(0, 0, true, double, 1, true, 1)         \
+    X(1, 0, true, double, 1, false, 2)        \
+    X(2, 0, false, double, 1, false, 2)       \
+    X(2, 0, false, double, 1, false, 1)       \
+    X(3, 0, false, double, 2, false, 1)       \
+    X(4, 0, true, float, 1, false, 2)         \
+    X(5, 0, false, float, 1, false, 2)        \
+    X(6, 0, false, float, 2, false, 2)        \
+    X(7, 1, true, double, 1, false, 2)        \
+    X(8, 1, false, double, 1, false, 2)       \
+    X(8, 1, false, double, 1, false, 1)       \
+    X(9, 1, false, double, 2, false, 1)
+#define MPCG_WIDE_RESUME_INSTANCES(X)         \
+    X(1, 0, true, double, 1)                  \
+    X(2, 0, false, double, 1)                 \
+    X(3, 0, false, double, 2)                 \
+    X(4, 0, true, float, 1)                   \
+    X(5, 0, false, float, 1)                  \
+    X(6, 0, false, float, 2)                  \
+    X(7, 1, true, double, 1)                  \
+    X(8, 1, false, double, 1)                 \
+    X(9, 1, false, double, 2)
+#define MPCG_DECL_SOLVE(g, M, S, T, NB, D, W) template <> const void* solve_kernel_fn<M, S, T, NB, D, W>();
+#define MPCG_DECL_RESUME(g, M, S, T, NB) template <> const void* resume_kernel_fn<M, S, T, NB>();
+MPCG_WIDE_SOLVE_INSTANCES(MPCG_DECL_SOLVE)
+MPCG_WIDE_RESUME_INSTANCES(MPCG_DECL_RESUME)
+#undef MPCG_DECL_SOLVE
+#undef MPCG_DECL_RESUME
+
+}  // namespace mpcg
+#endif
