@@ -2,6 +2,8 @@
 reference's MPC / LoadParams, the synthetic problem generator, sharding."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -89,3 +91,27 @@ def test_build_reads_kernel_resource_remarks():
     assert u[k] == {"VGPRs": 256, "ScratchSize [bytes/lane]": 128, "Occupancy [waves/SIMD]": 2,
                     "SGPRs Spill": 341, "LDS Size [bytes/block]": 4096}
     assert u["_ZN4mpcg11k_sched_keyElPKdPfPi"] == {"VGPRs": 12}
+
+
+def test_parallel_build_units_cover_every_instance_group():
+    """The parallel build compiles mpcg_wide_inst.hip once per group: the groups it names are
+    exactly the groups of the instance lists in mpcg_wide_kern.h (a group without a unit would
+    leave its kernels undefined at link time; a unit without instances is wasted), and every
+    solve instance's (model, split, type, blocks) has a resume instance (its parked problems)."""
+    import re
+
+    from mpc_ros_amd import build
+
+    text = open(os.path.join(build.CSRC, "mpcg_wide_kern.h")).read()
+    solve = re.findall(r"X\((\d+), (\d), (true|false), (double|float), (\d), (true|false), (\d)\)", text)
+    resume = re.findall(r"X\((\d+), (\d), (true|false), (double|float), (\d)\)", text)
+    assert solve and resume
+    groups = {int(g[0]) for g in solve} | {int(g[0]) for g in resume}
+    units = [u for u in build.compile_units() if u[0] == build.INST]
+    assert sorted(int(u[1][0].split("=")[1]) for u in units) == sorted(groups) == list(range(build.N_INST))
+    res = {tuple(r[1:]) for r in resume}
+    for _g, m, sp, ty, nb, _d, _w in solve:
+        assert (m, sp, ty, nb) in res
+    # every source of the library is compiled exactly once besides the instance groups
+    others = [u[0] for u in build.compile_units() if u[0] != build.INST]
+    assert sorted(others) == sorted(s for s in build.SOURCES if s != build.INST)

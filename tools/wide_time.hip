@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "mpcg_wide.hip"
@@ -111,6 +112,16 @@ int main(int argc, char** argv) {
     std::printf("B=%lld avg %.3f ms best %.3f ms -> %.3f M solves/s; iters mean %.3f max %d; success %d; lds %zu B\n",
                 (long long)B, tot / R, best, B / (tot / R) * 1e-3, (double)isum / B, imax, nok,
                 mpcg::wide_lds_bytes(P));
+    if (getenv("WT_TIMELINE")) {  // (variants whose write_out stores the wall clock in obj)
+        std::vector<double> ob(B);
+        CK(hipMemcpy(ob.data(), dobj, B * 8, hipMemcpyDeviceToHost));
+        std::sort(ob.begin(), ob.end());
+        const double t0 = ob[0], span = ob[B - 1] - ob[0];
+        std::printf("end-time spread %.3f ms (100 MHz clock);", span * 1e-5);
+        for (double q : {0.5, 0.9, 0.99, 0.999, 0.9999})
+            std::printf(" %.4g: %.3f", q, (ob[(int64_t)(q * (B - 1))] - t0) * 1e-5);
+        std::printf("\n");
+    }
     FILE* o = std::fopen(argv[2], "wb");
     if (o) {
         std::fwrite(u0.data(), 8, B * 2, o);
