@@ -46,8 +46,16 @@ namespace mpcg {
 // ds_write_b128 group hit distinct LDS banks; at a 64-byte stride they conflict 4-way.
 struct WideLayout {
     int N, cap, SS;  // SS: stage table stride (38; 42 with the bicycle's turn terms)
-    MPCG_HD WideLayout(int N_, int cap_, int model) : N(N_), cap(cap_), SS(model == 1 ? 42 : 38) {}
+    // KL: the gain records' stride in LDS -- KS, or 0 for the bicycle, whose gain records live
+    // in the problem's workspace (SP_KRG): its larger stage table would otherwise leave room
+    // for 6 problems per CU instead of 8
+    int KL;
+    MPCG_HD WideLayout(int N_, int cap_, int model)
+        : N(N_), cap(cap_), SS(model == 1 ? 42 : 38), KL(model == 1 ? 0 : KS) {}
     static constexpr int WS = 10, YS = 6, KS = 18;
+    // the iterate record of stage k: w (8), z_L (8), z_U (8), the step dw (8), 2 pad (one record
+    // instead of four 10-double arrays: 6 doubles per stage less)
+    static constexpr int RS = 34, RZL = 8, RZU = 16, RDW = 24;
     // stage table entries
     static constexpr int SA = 0;    // a[7]: non-trivial entries of A_k (Lin::jac)
     static constexpr int SDT = 7;   // dt
@@ -62,19 +70,19 @@ struct WideLayout {
     // column w: v/lf dt; dt for the differential drive), d(turn)/d(v) (A_hat column v:
     // w/lf dt; 0), and the (v, w) curvature of the Lagrangian (-(y_th + y_eth)/lf dt; 0)
     static constexpr int STW = 38, STV = 39, SHVD = 40;
-    MPCG_HD int W(int k) const { return WS * k; }
-    MPCG_HD int ZL(int k) const { return WS * (N + k); }
-    MPCG_HD int ZU(int k) const { return WS * (2 * N + k); }
-    MPCG_HD int DW(int k) const { return WS * (3 * N + k); }
-    MPCG_HD int Y(int k) const { return 4 * WS * N + YS * k; }
-    MPCG_HD int YP(int k) const { return (4 * WS + YS) * N + YS * k; }
-    MPCG_HD int KR(int k) const { return (4 * WS + 2 * YS) * N + KS * k; }  // K[0][0..7] K[1][0..7] kff[2]
-    MPCG_HD int ST(int k) const { return (4 * WS + 2 * YS + KS) * N + SS * k; }
+    MPCG_HD int W(int k) const { return RS * k; }
+    MPCG_HD int ZL(int k) const { return RS * k + RZL; }
+    MPCG_HD int ZU(int k) const { return RS * k + RZU; }
+    MPCG_HD int DW(int k) const { return RS * k + RDW; }
+    MPCG_HD int Y(int k) const { return RS * N + YS * k; }
+    MPCG_HD int YP(int k) const { return (RS + YS) * N + YS * k; }
+    MPCG_HD int KR(int k) const { return (RS + 2 * YS) * N + KS * k; }  // K[0][0..7] K[1][0..7] kff[2]
+    MPCG_HD int ST(int k) const { return (RS + 2 * YS + KL) * N + SS * k; }
     // scratch of the Riccati sweep: G^T of the stage, then M^T (M[r][c] at MS c + r) in
     // the same 8 columns, MS = 10 doubles apart (16-byte column reads of different
     // columns fall in different LDS banks); then P row-major
     static constexpr int MS = 10;
-    MPCG_HD int SCR() const { return (4 * WS + 2 * YS + KS + SS) * N; }
+    MPCG_HD int SCR() const { return (RS + 2 * YS + KL + SS) * N; }
     MPCG_HD int PSC() const { return SCR() + 8 * MS; }
     MPCG_HD int RSC() const { return SCR() + 8 * MS + 64; }  // row scales: ra[6] rb[6] 1.0 (+pad)
     MPCG_HD int ZB() const { return RSC() + 16; }            // 8 zeros (an absent column)
@@ -99,7 +107,10 @@ struct WideLayout {
     // SP_FLT, the restoration problem's at SP_FLTR
     static constexpr int FX = 448;
     MPCG_HD int SP_FLT() const { return 114 * N; }
-    MPCG_HD int spill() const { return 114 * N + 2 * FX; }
+    // the gain records of the bicycle (KL = 0): written by the Riccati sweep, read by the step
+    // recursion of the same Newton system
+    MPCG_HD int SP_KRG() const { return 114 * N + 2 * FX; }
+    MPCG_HD int spill() const { return SP_KRG() + (KL == 0 ? KS * N : 0); }
     // The feasibility-restoration phase (WideSolver<..., RESTO = true>, entered from the
     // original problem's line search): the original problem's LDS image while the
     // restoration problem uses the LDS (total()), the restoration problem's per-stage
@@ -1316,6 +1327,7 @@ struct WideSolver {
         // overwrite right after
         const int ga0 = t < 18 ? L.KR(0) + t : sm + MS * i + j;
         const int gak = t < 18 ? WideLayout::KS : 0;
+        T* const gk = spill + L.SP_KRG() + t;  // (the bicycle: the gain records in the workspace)
         // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
         const int hvj = j == 3 ? W_::SHVD : W_::SZERO, hvi = i == 3 ? W_::SHVD : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
@@ -1424,7 +1436,11 @@ struct WideSolver {
             wv.sync();  // this stage's reads of M are done
             // gains K (lanes 0..15: K[0][j], K[1][j]) and k (lanes 16, 17) in one store (the
             // other lanes' store lands in the G slot the next store overwrites)
-            st(ga0 + gak * k, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
+            if constexpr (MODEL == 1) {
+                if (t < 18) gk[WideLayout::KS * k] = i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1));
+            } else {
+                st(ga0 + gak * k, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
+            }
             st(sm + MS * i + j, gnext);
         }
         if constexpr (RESTO) {
@@ -1503,11 +1519,30 @@ struct WideSolver {
         }
     }
 
+    // stage k's gains K (2 x 8) and k_ff, written by the Riccati sweep: LDS, or (the bicycle)
+    // the workspace, ordered after the sweep's stores by forward_begin()
+    MPCG_HD void ld_gains(int k, T* K, T* kf) const {
+        if constexpr (MODEL == 1) {
+            const T* g = spill + L.SP_KRG() + WideLayout::KS * k;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) K[q] = g[q];
+            kf[0] = g[WideLayout::KF];
+            kf[1] = g[WideLayout::KF + 1];
+        } else {
+            ldv<16>(L.KR(k), K);
+            ldv<2>(L.KR(k) + WideLayout::KF, kf);
+        }
+    }
+    MPCG_HD void forward_begin() const {
+        wv.sync();
+        if constexpr (MODEL == 1) wv.gsync();  // (the gain records: written by other lanes)
+    }
+
     MPCG_HD Fwd forward(int mode) {
         if constexpr (RESTO) return forward_resto();
         if constexpr (NB == 2) return forward_blk(mode);
         const int t = wv.lane();  // (recomputed per phase: nothing lane-dependent is hoisted)
-        wv.sync();
+        forward_begin();
         // The step recursion ds_{k+1} = A ds_k + B du_k + d, du_k = kff + K ds_k runs
         // systolically: lane k holds stage k's records, every step every lane applies its
         // own stage map to the vector it holds and passes the result one lane up.  Lane 0
@@ -1519,8 +1554,7 @@ struct WideSolver {
         const int ks = SPLIT ? (t & 31) : t;  // the lane's stage
         T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
         if (ks < N - 1) {
-            ldv<16>(L.KR(ks), K);
-            ldv<2>(L.KR(ks) + WideLayout::KF, kf);
+            ld_gains(ks, K, kf);
             ldv<8>(L.ST(ks) + WideLayout::SA, a);
             ldv<6>(L.ST(ks) + WideLayout::SD, d);
             if constexpr (MODEL == 1)
@@ -1703,14 +1737,13 @@ struct WideSolver {
     // in each block).
     MPCG_HD Fwd forward_blk(int mode) {
         const int t = wv.lane();
-        wv.sync();
+        forward_begin();
         T xs[NB][6], dus[NB][2], xlast[8];
         for (int b = 0; b < NB; ++b) {
             const int ks = t + 64 * b;
             T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0;
             if (ks < N - 1) {
-                ldv<16>(L.KR(ks), K);
-                ldv<2>(L.KR(ks) + WideLayout::KF, kf);
+                ld_gains(ks, K, kf);
                 ldv<8>(L.ST(ks) + WideLayout::SA, a);
                 ldv<6>(L.ST(ks) + WideLayout::SD, d);
                 if constexpr (MODEL == 1)
@@ -2465,14 +2498,13 @@ struct WideSolver {
     // dp = (dy - r_p)/(Sigma_p + dw), dn = -(dy + r_n)/(Sigma_n + dw) and the step statistics.
     MPCG_HD Fwd forward_resto() {
         const int t = wv.lane();
-        wv.sync();
+        forward_begin();
         T xs[NB][8], dus[NB][2], xlast[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lin[NB][6];
         for (int b = 0; b < NB; ++b) {
             const int ks = t + 64 * b;
             T K[16], kf[2], a[8], d[6], twl = 0, tvl = 0, Mx[36], Nx[36], mv[6];
             if (ks < N - 1) {
-                ldv<16>(L.KR(ks), K);
-                ldv<2>(L.KR(ks) + WideLayout::KF, kf);
+                ld_gains(ks, K, kf);
                 ldv<8>(L.ST(ks) + WideLayout::SA, a);
                 ldv<6>(L.ST(ks) + WideLayout::SD, d);
                 if constexpr (MODEL == 1)
@@ -2844,6 +2876,21 @@ struct WideSolver {
         const int t = wv.lane();
         wv.sync();
         for (int e = t; e < n; e += 64) st(lds0 + e, (T)spill[sp0 + e]);
+        wv.sync();
+    }
+    // the same for the fields [off, off + len) of every stage's iterate record (len N elements
+    // at sp0, stage-major)
+    template <int off, int len>
+    MPCG_HD void rec_out(int sp0) {
+        const int t = wv.lane();
+        wv.sync();
+        for (int e = t; e < len * N; e += 64) spill[sp0 + e] = ld(WideLayout::RS * (e / len) + off + e % len);
+    }
+    template <int off, int len>
+    MPCG_HD void rec_in(int sp0) {
+        const int t = wv.lane();
+        wv.sync();
+        for (int e = t; e < len * N; e += 64) st(WideLayout::RS * (e / len) + off + e % len, (T)spill[sp0 + e]);
         wv.sync();
     }
 
@@ -3419,7 +3466,7 @@ struct WideSolver {
             last_mu() = mu;
         }
         if (!RESTO && P.acceptable_iter > 0 && cur_acceptable) {
-            spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
+            rec_out<0, 8>(L.SP_ACC());
             have_acc = 1;
         }
         const T phik = phi_cur();
@@ -3490,7 +3537,7 @@ struct WideSolver {
         if (wv.uni(!ls_eval_error && ls_alpha == ls_alpha_max && theta <= tr_theta) && P.max_soc > 0) {
             // FilterLSAcceptor::TrySecondOrderCorrection from the same factorisation; the
             // Newton direction waits in the spill area
-            spill_out(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+            rec_out<WideLayout::RDW, 8>(L.SP_SOC());
             spill_out(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
             xcopy(true, WideLayout::XDP, 36, 12);
             soc_count = 0;
@@ -3509,7 +3556,7 @@ struct WideSolver {
             soc_theta_old() = soc_theta_trial();
             return set_op(OP_SOCRHS, K_SOCRHS);
         }
-        spill_in(L.SP_SOC(), L.DW(0), WideLayout::WS * N);
+        rec_in<WideLayout::RDW, 8>(L.SP_SOC());
         spill_in(L.SP_SOC() + WideLayout::WS * N, L.YP(0), WideLayout::YS * N);
         xcopy(false, WideLayout::XDP, 36, 12);
         ls_alpha *= (T)0.5;
@@ -3554,7 +3601,7 @@ struct WideSolver {
     }
     MPCG_HD void start_watchdog(const Fwd& F) {
         in_wd = 1;
-        spill_out(L.SP_WD(), 0, 52 * N);  // W, ZL, ZU, DW, Y, YP
+        spill_out(L.SP_WD(), 0, (WideLayout::RS + 2 * WideLayout::YS) * N);  // W, ZL, ZU, DW records, Y, YP
         xcopy(true, WideLayout::XP, 0, 36);  // (RESTO: p, n, z_p, z_n, dp, dn)
         wd_trial_iter = 0;
         wd_alpha_test() = F.amax_p;
@@ -3566,7 +3613,7 @@ struct WideSolver {
     // back to the watchdog's stored iterate and direction; its statistics next
     MPCG_HD int stop_watchdog() {
         in_wd = 0;
-        spill_in(L.SP_WD(), 0, 52 * N);
+        spill_in(L.SP_WD(), 0, (WideLayout::RS + 2 * WideLayout::YS) * N);
         xcopy(false, WideLayout::XP, 0, 36);
         wd_short = 0;
         c_ok = 0;
@@ -3600,7 +3647,7 @@ struct WideSolver {
     }
     MPCG_HD int k_soft_pd0() {
         soft_ec() = pd_val;
-        spill_out(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);  // W, ZL, ZU
+        rec_out<0, 24>(L.SP_SOFT());  // W, ZL, ZU
         spill_out(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
         xcopy(true, WideLayout::XP, 48, 24);  // (RESTO: p, n, z_p, z_n)
         accept_all(wv.lane(), true, soft_a(), soft_a(), false);
@@ -3612,7 +3659,7 @@ struct WideSolver {
             clamp_all();  // kappa_sigma correction of the accepted multipliers
             return soft_done(true, false);
         }
-        spill_in(L.SP_SOFT(), 0, 3 * WideLayout::WS * N);
+        rec_in<0, 24>(L.SP_SOFT());
         spill_in(L.SP_SOFT() + 3 * WideLayout::WS * N, L.Y(0), WideLayout::YS * N);
         xcopy(false, WideLayout::XP, 48, 24);
         return soft_done(false, false);
@@ -3667,7 +3714,7 @@ struct WideSolver {
             // almost feasible: the last acceptable iterate, if any, is the result
             if (wv.uni(theta <= (T)1e-2 * (T)P.tol)) {
                 if (have_acc) {
-                    spill_in(L.SP_ACC(), 0, WideLayout::WS * N);
+                    rec_in<0, 8>(L.SP_ACC());
                     return IPM_ACCEPTABLE;
                 }
                 return IPM_RESTORATION_FAILURE;
@@ -3688,7 +3735,7 @@ struct WideSolver {
             last_mu() = mu;
         }
         if (P.acceptable_iter > 0 && cur_acceptable) {
-            spill_out(L.SP_ACC(), 0, WideLayout::WS * N);
+            rec_out<0, 8>(L.SP_ACC());
             have_acc = 1;
         }
         if (in_wd) {  // the watchdog's stored iterate and direction, searched without skipping
