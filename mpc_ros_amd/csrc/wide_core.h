@@ -95,9 +95,10 @@ struct WideLayout {
     MPCG_HD int total() const { return PRB() + 12; }
     // Per-wavefront HBM workspace (elements of T) of the rare paths, one per resident
     // wavefront (mpcg_wide.hip claims a slot per problem).  The watchdog's stored iterate
-    // and direction (LDS [W(0), YP(N)) = 52N), the last acceptable iterate (W: 10N), the
-    // Newton direction kept while second-order corrections are tried (DW, YP: 16N), the
-    // iterate kept while a soft-restoration step is evaluated (W, ZL, ZU, Y: 36N).
+    // and direction (LDS [W(0), YP(N)) = 46N of a 52N region), the last acceptable iterate
+    // (w: 8N of 10N), the Newton direction kept while second-order corrections are tried (DW,
+    // YP: 14N of 16N), the iterate kept while a soft-restoration step is evaluated (w, z_L,
+    // z_U, y: 30N of 36N).
     MPCG_HD int SP_WD() const { return 0; }
     MPCG_HD int SP_ACC() const { return 52 * N; }
     MPCG_HD int SP_SOC() const { return 62 * N; }
