@@ -98,9 +98,9 @@ static const void* wide_kernel(const IpmParams& P, int64_t B) {
     const int nb = P.N > 64 ? 2 : 1;
     if (P.N > 128) return nullptr;
     if (f32 && P.model != 0) return nullptr;  // (fp32: the differential drive)
-    if (f32)
+    if (f32)  // (N <= 64: 3 wavefronts per SIMD, mpcg_wide_kern.h)
         return nb == 2 ? sk<0, false, float, 2, false, 2>()
-             : split ? sk<0, true, float, 1, false, 2>() : sk<0, false, float, 1, false, 2>();
+             : split ? sk<0, true, float, 1, false, 3>() : sk<0, false, float, 1, false, 3>();
     const bool one = wide_lds_bytes(P) > 32768;
     if (P.model == 1)
         return nb == 2 ? sk<1, false, double, 2, false, 1>()

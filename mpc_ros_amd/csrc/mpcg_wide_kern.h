@@ -103,8 +103,11 @@ __device__ __forceinline__ void release_slot(int32_t* flags, int s) {
 template <class Solver>
 __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked);
 
-// WPE: wavefronts per SIMD the register allocation is for -- 2 (256 VGPRs), or 1 (512) for
-// the instances whose LDS per problem allows at most 4 problems per CU anyway (wide_kernel)
+// WPE: wavefronts per SIMD the register allocation is for -- 2 (256 VGPRs), 1 (512) for the
+// instances whose LDS per problem allows at most 4 problems per CU anyway (wide_kernel), or
+// 3 (168 VGPRs) for the fp32 solver (N <= 64), whose LDS per problem leaves room for more
+// than 8 problems per CU (N = 20: 9.5 KB, 12 per CU; N = 40: 14.8 KB, 11): with 68 VGPRs
+// spilled the split instance is still 13 % faster than at 2 per SIMD
 template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_solve_wide(WideArgs a) {
     if ((int64_t)blockIdx.x >= a.B) return;
@@ -262,8 +265,8 @@ const void* resume_kernel_fn();
     X(2, 0, false, double, 1, false, 2)       \
     X(2, 0, false, double, 1, false, 1)       \
     X(3, 0, false, double, 2, false, 1)       \
-    X(4, 0, true, float, 1, false, 2)         \
-    X(5, 0, false, float, 1, false, 2)        \
+    X(4, 0, true, float, 1, false, 3)         \
+    X(5, 0, false, float, 1, false, 3)        \
     X(6, 0, false, float, 2, false, 2)        \
     X(7, 1, true, double, 1, false, 2)        \
     X(8, 1, false, double, 1, false, 2)       \

@@ -46,12 +46,12 @@ namespace mpcg {
 // ds_write_b128 group hit distinct LDS banks; at a 64-byte stride they conflict 4-way.
 struct WideLayout {
     int N, cap, SS;  // SS: stage table stride (38; 42 with the bicycle's turn terms)
-    // KL: the gain records' stride in LDS -- KS, or 0 for the bicycle, whose gain records live
-    // in the problem's workspace (SP_KRG): its larger stage table would otherwise leave room
-    // for 6 problems per CU instead of 8
+    // KL: the gain records' stride in LDS -- KS, or 0 for the bicycle and every N > 32, whose
+    // gain records live in the problem's workspace (SP_KRG): more problems per CU (bicycle
+    // N = 25: 8 instead of 6; fp32 N = 40: 11 instead of 9; fp64 N = 64: 3 instead of 2)
     int KL;
     MPCG_HD WideLayout(int N_, int cap_, int model)
-        : N(N_), cap(cap_), SS(model == 1 ? 42 : 38), KL(model == 1 ? 0 : KS) {}
+        : N(N_), cap(cap_), SS(model == 1 ? 42 : 38), KL(model == 1 || N_ > 32 ? 0 : KS) {}
     static constexpr int WS = 10, YS = 6, KS = 18;
     // the iterate record of stage k: w (8), z_L (8), z_U (8), the step dw (8), 2 pad (one record
     // instead of four 10-double arrays: 6 doubles per stage less)
@@ -108,8 +108,8 @@ struct WideLayout {
     // SP_FLT, the restoration problem's at SP_FLTR
     static constexpr int FX = 448;
     MPCG_HD int SP_FLT() const { return 114 * N; }
-    // the gain records of the bicycle (KL = 0): written by the Riccati sweep, read by the step
-    // recursion of the same Newton system
+    // the gain records when KL = 0: written by the Riccati sweep, read by the step recursion of
+    // the same Newton system
     MPCG_HD int SP_KRG() const { return 114 * N + 2 * FX; }
     MPCG_HD int spill() const { return SP_KRG() + (KL == 0 ? KS * N : 0); }
     // The feasibility-restoration phase (WideSolver<..., RESTO = true>, entered from the
@@ -1328,7 +1328,8 @@ struct WideSolver {
         // overwrite right after
         const int ga0 = t < 18 ? L.KR(0) + t : sm + MS * i + j;
         const int gak = t < 18 ? WideLayout::KS : 0;
-        T* const gk = spill + L.SP_KRG() + t;  // (the bicycle: the gain records in the workspace)
+        T* const gk = spill + L.SP_KRG() + t;  // (KL = 0: the gain records in the workspace)
+        const bool khbm = kr_hbm();
         // (v, w) curvature of the Lagrangian: S_tilde(0, 3) (bicycle; zero otherwise)
         const int hvj = j == 3 ? W_::SHVD : W_::SZERO, hvi = i == 3 ? W_::SHVD : W_::SZERO;
         // Q_hat(i, j): diagonal, constraint curvature
@@ -1437,7 +1438,7 @@ struct WideSolver {
             wv.sync();  // this stage's reads of M are done
             // gains K (lanes 0..15: K[0][j], K[1][j]) and k (lanes 16, 17) in one store (the
             // other lanes' store lands in the G slot the next store overwrites)
-            if constexpr (MODEL == 1) {
+            if (khbm) {
                 if (t < 18) gk[WideLayout::KS * k] = i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1));
             } else {
                 st(ga0 + gak * k, i == 0 ? K0 : (i == 1 ? K1 : (j == 0 ? kf0 : kf1)));
@@ -1520,10 +1521,18 @@ struct WideSolver {
         }
     }
 
-    // stage k's gains K (2 x 8) and k_ff, written by the Riccati sweep: LDS, or (the bicycle)
-    // the workspace, ordered after the sweep's stores by forward_begin()
+    // the gain records are in the workspace (WideLayout::KL = 0; never for the diff-drive's
+    // split instances, N <= 32)
+    MPCG_HD bool kr_hbm() const {
+        if constexpr (MODEL == 0 && SPLIT)
+            return false;
+        else
+            return L.KL == 0;
+    }
+    // stage k's gains K (2 x 8) and k_ff, written by the Riccati sweep: LDS, or the workspace,
+    // ordered after the sweep's stores by forward_begin()
     MPCG_HD void ld_gains(int k, T* K, T* kf) const {
-        if constexpr (MODEL == 1) {
+        if (kr_hbm()) {
             const T* g = spill + L.SP_KRG() + WideLayout::KS * k;
 #pragma unroll
             for (int q = 0; q < 16; ++q) K[q] = g[q];
@@ -1536,7 +1545,7 @@ struct WideSolver {
     }
     MPCG_HD void forward_begin() const {
         wv.sync();
-        if constexpr (MODEL == 1) wv.gsync();  // (the gain records: written by other lanes)
+        if (kr_hbm()) wv.gsync();  // (the gain records: written by other lanes)
     }
 
     MPCG_HD Fwd forward(int mode) {
