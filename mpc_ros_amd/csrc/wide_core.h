@@ -50,8 +50,10 @@ struct WideLayout {
     // gain records live in the problem's workspace (SP_KRG): more problems per CU (bicycle
     // N = 25: 8 instead of 6; fp32 N = 40: 11 instead of 9; fp64 N = 64: 3 instead of 2)
     int KL;
-    MPCG_HD WideLayout(int N_, int cap_, int model)
-        : N(N_), cap(cap_), SS(model == 1 ? 42 : 38), KL(model == 1 || N_ > 32 ? 0 : KS) {}
+    // (kl >= 0: the caller knows KL at compile time -- the diff-drive split solver, N <= 32 --
+    // and the layout's offsets fold to constants)
+    MPCG_HD WideLayout(int N_, int cap_, int model, int kl = -1)
+        : N(N_), cap(cap_), SS(model == 1 ? 42 : 38), KL(kl >= 0 ? kl : (model == 1 || N_ > 32 ? 0 : KS)) {}
     static constexpr int WS = 10, YS = 6, KS = 18;
     // the iterate record of stage k: w (8), z_L (8), z_U (8), the step dw (8), 2 pad (one record
     // instead of four 10-double arrays: 6 doubles per stage less)
@@ -267,7 +269,7 @@ struct WideSolver {
     bool mu_done = false;
 
     MPCG_HD WideSolver(const IpmParams& P_, const IpmProblem<T>& pr_, const WV& wv_, T* spill_)
-        : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf),
+        : P(P_), pr(pr_), wv(wv_), L(P_.N, P_.filter_cap, MODEL, MODEL == 0 && SPLIT ? WideLayout::KS : -1), N(P_.N), t(wv_.t), dt((T)P_.dt), lf((T)P_.lf),
           spill(spill_) {}
 
     // ------------------------------------------------------ the model
