@@ -89,9 +89,11 @@ static const void* resume_kernel(const IpmParams& P) {
 // null if none.  An fp64 problem of more than 32 KB of LDS (N >= 35; every N > 64) leaves
 // room for at most 4 problems per CU (160 KB), one wavefront per SIMD: its instance is
 // register-allocated for one (512 VGPRs, no spills) instead of two.
-// A batch the device holds at one wavefront per SIMD (B <= kLoneBatch: 4 x 256 CUs) runs
-// the benchmark configuration's instance allocated for one wavefront per SIMD as well.
-constexpr int64_t kLoneBatch = 1024;
+// A small batch (B <= kLoneBatch) runs the benchmark configuration's instance allocated for
+// one wavefront per SIMD as well: its time is set by its longest problem at the
+// lone-wavefront rate, which the 512-VGPR allocation (no spills) shortens (B = 4,096, the
+// BASELINE's configs[1]: 3.02 -> 2.93 ms; B = 1,024 is held at one wavefront per SIMD).
+constexpr int64_t kLoneBatch = 4096;
 static const void* wide_kernel(const IpmParams& P, int64_t B) {
     const bool split = P.N <= 32;
     const bool f32 = P.precision == 1;
