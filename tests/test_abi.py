@@ -96,17 +96,17 @@ def test_workspace_bytes(libmpcg):
     flags and counters (slot flags, park count/taken/done, park indices, park ready flags)
     precede them.  N = 20: a slot is 114N + 2*448 = 3176 doubles (rare-path copies and the
     filter entries beyond the 64 held in LDS) rounded to whole 128-byte lines, 3184; a park
-    entry 32 + 2492 (LDS image) + 10644 (a slot, 2492 for the original problem's image, 204N
-    of restoration records and the restoration filter's overflow) = 13168 (whole lines);
+    entry 32 + 2372 (LDS image) + 10524 (a slot, 2372 for the original problem's image, 204N
+    of restoration records and the restoration filter's overflow) = 12928 (whole lines);
     without a GPU the slot count falls back to 4096."""
     from mpc_ros_amd import _lib
 
     p = _lib.MpcgParams()
     libmpcg.mpcg_params_plugin_default(C.byref(p))
     b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
-    assert b1 == 4 * 256 + (8 * 3184 + 13168) * 8
+    assert b1 == 4 * 256 + (8 * 3184 + 12928) * 8
     b2 = libmpcg.mpcg_workspace_bytes(C.byref(p), 2)
-    assert b2 == 4 * 256 + (16 * 3184 + 2 * 13168) * 8
+    assert b2 == 4 * 256 + (16 * 3184 + 2 * 12928) * 8
     big = libmpcg.mpcg_workspace_bytes(C.byref(p), 65536)
     assert big < 65536 * 3184 * 8 // 4  # (bounded by residency, not by B)
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
