@@ -4,7 +4,7 @@
 // dispatcher in mpcg_wide.hip reaches them through solve_kernel_fn / resume_kernel_fn.
 //
 // One workgroup = one wavefront = one problem; the problem's whole state lives in
-// the workgroup's LDS (WideLayout: 19.9 KB at N = 20, i.e. 8 problems resident per
+// the workgroup's LDS (WideLayout: 19.0 KB at N = 20, i.e. 8 problems resident per
 // CU).  Workgroups are dispatched by the hardware as CUs free up, so a slow problem
 // occupies one wavefront slot while the rest of the batch streams past it.
 #ifndef MPCG_WIDE_KERN_H
