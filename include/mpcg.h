@@ -68,16 +68,21 @@ typedef struct mpcg_params {
     /* Ipopt 3.12 defaults unless changed */
     double tol;               /* 1e-8 */
     int32_t max_iter;         /* 3000 */
-    int32_t filter_cap;       /* non-dominated filter entries kept per problem (64; the oldest is
-                                 dropped beyond -- Ipopt's filter is unbounded) */
+    int32_t filter_cap;       /* filter entries held in LDS per problem (64); 448 more are kept in
+                                 the HBM workspace, so the oldest entry is dropped only beyond
+                                 filter_cap + 448 non-dominated entries (counted in diag[:, 1];
+                                 Ipopt's filter is unbounded) */
     double bound_relax_factor;/* 1e-8 */
     double mu_init;           /* 0.1 */
     double wheelbase;         /* model 1 only: Lf [m] */
     /* "max_cpu_time" (the reference sets 0.5 s, mpc_planner.cpp:368): applied as the number of
-     * iterations the reference's Solve affords in that time at this horizon (CppAD taping and
-     * per-iteration derivative cost measured in the survey: 1.52 ms + 0.225 ms/iteration at
-     * N = 20), so that results are deterministic; beyond it the status is 14 (unknown) with the
-     * last iterate.  >= 1e6: no budget (Ipopt's "no limit"). */
+     * iterations the reference's Solve affords in that time at this horizon, so that results
+     * are deterministic: (max_cpu_time - CppAD taping) / (CppAD derivative evaluations + Ipopt's
+     * own iteration work) -- taping and derivatives measured in the survey (1.52 ms and
+     * 0.225 ms per iteration at N = 20), Ipopt's KKT factorisation, solve and line search
+     * calibrated at 5.14 us per stage (0.103 ms at N = 20): 1,520 iterations at N = 20, 737 at
+     * N = 40.  Beyond it the status is 14 (unknown) with the last iterate.  >= 1e6: no budget
+     * (Ipopt's "no limit"). */
     double max_cpu_time;
     /* Ipopt 3.12 defaults (the reference leaves them untouched) */
     double acceptable_tol;             /* 1e-6 */
@@ -137,12 +142,22 @@ int mpcg_create(int device, mpcg_handle** out);
 void mpcg_destroy(mpcg_handle* h);
 int mpcg_set_params(mpcg_handle* h, const mpcg_params* p);
 int mpcg_get_params(const mpcg_handle* h, mpcg_params* p);
-/* Device workspace for B problems (bytes): one slot per wavefront the GPU holds resident
- * (not per problem: the rare solver paths' copies and the restoration phase's records), the
- * park area of problems that enter the restoration phase (max(256, B/256) entries), and the
- * solve-order buffers; reserve it ahead of graph capture. */
+/* Device workspace for B problems (bytes): 4 slots per wavefront the GPU holds resident
+ * (not per problem: the rare solver paths' copies), the park area of problems that enter the
+ * restoration phase (max(256, B/128) entries, at most B; each holds the problem's state and
+ * the restoration phase's records), the park-area overflow list (8 B per problem where the
+ * area can overflow), and the solve-order buffers (B > 2048); reserve it ahead of graph
+ * capture (a solve that must grow it allocates and synchronises the device). */
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B);
 int mpcg_reserve(mpcg_handle* h, int64_t B);
+/* Park-area entries of the handle's solves (0 = the default max(256, B/128)).  A problem that
+ * enters the restoration phase while every entry is taken goes to an overflow list and is
+ * solved again from the start after the batch (the same iterates, diag[:, 2] = 2): results do
+ * not depend on the capacity, only the tail does.  A tuning and test knob. */
+int mpcg_set_park_capacity(mpcg_handle* h, int64_t cap);
+/* The solver kernel instance the handle's last solve launched, "k_solve_wide<model, split,
+ * type, stage blocks, default options, waves per SIMD>" ("" before the first solve). */
+const char* mpcg_last_kernel(const mpcg_handle* h);
 
 /* Batched solve, host buffers, synchronous (copies in, solves, copies out).
  *   state  [B][6]  x, y, theta, v, cte, etheta   (MPC::Solve `state`)
@@ -165,7 +180,8 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
  * may be NULL): restoration phases entered, filter entries dropped beyond its capacity
  * (filter_cap in LDS plus 448 in the workspace; Ipopt's filter is unbounded, so any nonzero
  * value marks a solve that may differ from Ipopt's), 1 if the problem was continued by the
- * parked-problem kernel, the most filter entries held at once (the original problem). */
+ * parked-problem kernel (2 if it was solved again after a park-area overflow, 0 otherwise), the
+ * most filter entries held at once (the original problem). */
 int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
                   int32_t* status, double* obj, int32_t* iters, int32_t* diag);
 int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,

@@ -114,7 +114,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     return LIB
 
 
-RESOURCES = os.path.join(ROOT, "profiles", "r3", "resources.json")
+RESOURCES = os.path.join(ROOT, "profiles", "r4", "resources.json")
 
 
 def demangle(names):

@@ -77,6 +77,7 @@ struct IpmParams {
     int cpu_iter_budget;                // max_cpu_time as iterations (-1 = none): status UNKNOWN beyond
     int precision;                      // 0: fp64 (Ipopt's); 1: fp32 solver (differential drive)
     int no_resto;                       // 1: RESTORATION_FAILURE where the restoration phase would start
+    int park_cap;                       // park-area entries (0: max(256, B / 128); host side only)
 };
 
 // The Ipopt 3.12 options the reference leaves at their defaults (mpc_planner.cpp:356-368:

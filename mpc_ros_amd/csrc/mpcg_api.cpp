@@ -60,6 +60,10 @@ struct mpcg_handle {
     hipStream_t last_stream = nullptr;
     hipEvent_t last_ev = nullptr;
     bool have_last = false;
+    // the solver kernel instance the last solve launched (mpcg_last_kernel)
+    const char* last_kernel = "";
+    // park-area entries (0: the default, max(256, B / 128))
+    int64_t park_cap = 0;
 };
 
 #ifndef MPCG_BUILD_ID
@@ -342,8 +346,14 @@ int mpcg_get_params(const mpcg_handle* h, mpcg_params* p) {
     return 0;
 }
 
+static mpcg::IpmParams handle_ipm(const mpcg_handle* h) {
+    mpcg::IpmParams P = to_ipm(h->params);
+    P.park_cap = (int)h->park_cap;
+    return P;
+}
+
 static int ensure_spill(mpcg_handle* h, int64_t B) {
-    const size_t need = mpcg::wide_spill_bytes(to_ipm(h->params), B);
+    const size_t need = mpcg::wide_spill_bytes(handle_ipm(h), B);
     if (need <= h->spill_bytes) return 0;
     hipSetDevice(h->device);
     if (h->d_spill) {
@@ -437,7 +447,7 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;  // NULL = the null stream, as in HIP
-    const mpcg::IpmParams P = to_ipm(h->params);
+    const mpcg::IpmParams P = handle_ipm(h);
     if (!wave_fits(P)) return fail(-1, "STEPS must be <= 128 (the problem state must fit the CU's 160 KiB of LDS)");
     rc = ensure_spill(h, B);
     if (rc) return rc;
@@ -457,7 +467,8 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
         order = ord;
     }
     e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, d_diag, order,
-                                (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join);
+                                (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join,
+                                &h->last_kernel);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     return record_on(h, s);
 }
@@ -589,6 +600,15 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
     e = mpcg::launch_post(B, h->params.dt, h->params.ref_v, d_vel, u0, d_cmd, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "post-processing launch");
     return record_on(h, (hipStream_t)stream);
+}
+
+const char* mpcg_last_kernel(const mpcg_handle* h) { return h ? h->last_kernel : ""; }
+
+int mpcg_set_park_capacity(mpcg_handle* h, int64_t cap) {
+    if (!h) return fail(-1, "null handle");
+    if (cap < 0 || cap > (int64_t)1 << 30) return fail(-1, "park capacity must be in [0, 2^30]");
+    h->park_cap = cap;
+    return 0;
 }
 
 int mpcg_synchronize(mpcg_handle* h) {

@@ -25,7 +25,10 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
                              const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
                              hipStream_t aux = nullptr,
-                             hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
+                             hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
+                             const char** kernel_name = nullptr);
+// park-area capacity of a batch of B (problems that enter the restoration phase)
+int64_t wide_park_cap(const IpmParams& P, int64_t B);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the
 // launch that writes the workgroup -> problem map into `buf` (returned in *order).
 size_t wide_sched_bytes(int64_t B);

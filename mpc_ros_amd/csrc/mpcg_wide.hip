@@ -54,14 +54,16 @@ size_t wide_lds_bytes(const IpmParams& P) {
 // The instances (solve_kernel_fn / resume_kernel_fn, mpcg_wide_inst.hip).  A diagnostic
 // build with MPCG_HEADLINE_ONLY links only the benchmark configuration's group (tools/).
 template <int M, bool S, class T, int NB, bool D, int W>
-static const void* sk() {
+static WideInst sk(const char* name) {
 #ifdef MPCG_HEADLINE_ONLY
     if constexpr (!(M == 0 && S && sizeof(T) == 8 && NB == 1 && D))
-        return nullptr;
+        return WideInst{nullptr, name};
     else
 #endif
-        return solve_kernel_fn<M, S, T, NB, D, W>();
+        return WideInst{solve_kernel_fn<M, S, T, NB, D, W>(), name};
 }
+// (the instance and its name: mpcg_last_kernel() reports the name of the one a solve launched)
+#define SK(M, S, T, NB, D, W) sk<M, S, T, NB, D, W>("k_solve_wide<" #M "," #S "," #T "," #NB "," #D "," #W ">")
 template <int M, bool S, class T, int NB>
 static const void* rk() {
 #ifdef MPCG_HEADLINE_ONLY
@@ -94,38 +96,48 @@ static const void* resume_kernel(const IpmParams& P) {
 // lone-wavefront rate, which the 512-VGPR allocation (no spills) shortens (B = 4,096, the
 // BASELINE's configs[1]: 3.02 -> 2.93 ms; B = 1,024 is held at one wavefront per SIMD).
 constexpr int64_t kLoneBatch = 4096;
-static const void* wide_kernel(const IpmParams& P, int64_t B) {
+WideInst wide_kernel(const IpmParams& P, int64_t B) {
     const bool split = P.N <= 32;
     const bool f32 = P.precision == 1;
     const int nb = P.N > 64 ? 2 : 1;
-    if (P.N > 128) return nullptr;
-    if (f32 && P.model != 0) return nullptr;  // (fp32: the differential drive)
+    if (P.N > 128) return WideInst{nullptr, ""};
+    if (f32 && P.model != 0) return WideInst{nullptr, ""};  // (fp32: the differential drive)
     if (f32)  // (N <= 64: 3 wavefronts per SIMD, mpcg_wide_kern.h)
-        return nb == 2 ? sk<0, false, float, 2, false, 2>()
-             : split ? sk<0, true, float, 1, false, 3>() : sk<0, false, float, 1, false, 3>();
+        return nb == 2 ? SK(0, false, float, 2, false, 2)
+             : split ? SK(0, true, float, 1, false, 3) : SK(0, false, float, 1, false, 3);
     const bool one = wide_lds_bytes(P) > 32768;
     if (P.model == 1)
-        return nb == 2 ? sk<1, false, double, 2, false, 1>()
-             : split ? sk<1, true, double, 1, false, 2>()
-             : one   ? sk<1, false, double, 1, false, 1>()
-                     : sk<1, false, double, 1, false, 2>();
+        return nb == 2 ? SK(1, false, double, 2, false, 1)
+             : split ? SK(1, true, double, 1, false, 2)
+             : one   ? SK(1, false, double, 1, false, 1)
+                     : SK(1, false, double, 1, false, 2);
     if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
-        return B <= kLoneBatch ? sk<0, true, double, 1, true, 1>() : sk<0, true, double, 1, true, 2>();
-    return nb == 2 ? sk<0, false, double, 2, false, 1>()
-         : split ? sk<0, true, double, 1, false, 2>()
-         : one   ? sk<0, false, double, 1, false, 1>()
-                 : sk<0, false, double, 1, false, 2>();
+        return B <= kLoneBatch ? SK(0, true, double, 1, true, 1) : SK(0, true, double, 1, true, 2);
+    return nb == 2 ? SK(0, false, double, 2, false, 1)
+         : split ? SK(0, true, double, 1, false, 2)
+         : one   ? SK(0, false, double, 1, false, 1)
+                 : SK(0, false, double, 1, false, 2);
+}
+
+// XCDs of the current device (HW_REG_XCC_ID partitions of the workspace slots); 8 on an
+// MI355X in SPX mode, fewer on a partitioned device
+int device_xccs() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess ||
+        n < 1)
+        return kXcds;
+    return n > 16 ? 16 : n;
 }
 
 // Workspace slots for a batch of B: four times the wavefronts the device can hold resident at
 // once (occupancy of the instance at its LDS size times the CUs), at most B (at least 32 per
-// XCD), in kXcds equal partitions.  A wavefront claims slot blockIdx mod the partition size
+// XCD), in one equal partition per XCD (device_xccs).  A wavefront claims slot blockIdx mod the partition size
 // in its XCD's partition, or the next free one: with the margin, a slow problem still
 // holding a slot rarely makes a later wavefront probe further.
 int64_t wide_slots(const IpmParams& P, int64_t B) {
     if (B <= 0) return 0;
     int64_t n = 4096;  // (fallback if the runtime cannot say)
-    const void* fn = wide_kernel(P, B);
+    const void* fn = wide_kernel(P, B).fn;
     int dev = 0, cus = 0, per = 0;
     if (fn && hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
@@ -134,10 +146,11 @@ int64_t wide_slots(const IpmParams& P, int64_t B) {
         cus > 0)
         n = 4 * (int64_t)per * cus;
     n = n < B ? n : B;
-    int64_t part = (n + kXcds - 1) / kXcds;
+    const int nx = device_xccs();
+    int64_t part = (n + nx - 1) / nx;
     const int64_t floor_ = B < 32 ? B : 32;
     part = part > floor_ ? part : floor_;
-    return part * kXcds;
+    return part * nx;
 }
 // a slot's elements: WideLayout::spill() rounded up to whole 128-byte lines
 static int64_t slot_elems(const IpmParams& P) {
@@ -147,11 +160,17 @@ static int64_t slot_elems(const IpmParams& P) {
 }
 static size_t slot_flag_bytes(int64_t nslots) { return ((size_t)nslots * sizeof(int32_t) + 255) & ~(size_t)255; }
 // the park area: problems that enter the restoration phase (rare: ~5e-5 of the infinity set at
-// N = 20, 5e-4 at N = 40, ~4e-3 with the fp32 solver at N = 40); beyond its capacity (B / 128,
-// at least 256) a problem ends with restoration_failure
-int64_t wide_park_cap(int64_t B) {
-    const int64_t c = B / 128 > 256 ? B / 128 : 256;
+// N = 20, 5e-4 at N = 40, ~4e-3 with the fp32 solver at N = 40); its capacity is B / 128, at
+// least 256 (P.park_cap > 0: that many, mpcg_set_park_capacity).  Beyond it a problem goes to
+// the overflow list and is solved again from the start after the drain.
+int64_t wide_park_cap(const IpmParams& P, int64_t B) {
+    int64_t c = B / 128 > 256 ? B / 128 : 256;
+    if (P.park_cap > 0) c = P.park_cap;
     return c < B ? c : B;
+}
+// the overflow list: one index per problem (only where the park area can overflow)
+static size_t ovf_bytes(const IpmParams& P, int64_t B) {
+    return wide_park_cap(P, B) < B ? ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255 : 0;
 }
 static size_t park_elems(const IpmParams& P) {
     const WideLayout L(P.N, P.filter_cap, P.model);
@@ -159,9 +178,9 @@ static size_t park_elems(const IpmParams& P) {
     return (n + per_line - 1) / per_line * per_line;
 }
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
-    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
+    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) + slot_flag_bytes(pc) +
-           (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns +
+           ovf_bytes(P, B) + (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns +
            park_elems(P) * elem_bytes(P) * (size_t)pc;
 }
 
@@ -178,12 +197,14 @@ static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 6553
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
                              const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
-                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
+                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join, const char** kernel_name) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = wide_lds_bytes(P);
-    const void* fn = wide_kernel(P, B);
+    const WideInst inst = wide_kernel(P, B);
+    const void* fn = inst.fn;
     if (!fn) return hipErrorInvalidValue;
+    if (kernel_name) *kernel_name = inst.name;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -191,28 +212,31 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // the workspace (wide_spill_bytes): slot flags | park count, taken, done (256 B) | park
-    // indices | park ready flags | slots | park area
-    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(B);
+    // the workspace (wide_spill_bytes): slot flags | counters: park count, taken, done,
+    // started, overflow count, overflow taken (256 B) | park indices | park ready flags |
+    // overflow list | slots | park area
+    const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     if (ns < 1 || wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
     char* w = (char*)spill;
     int32_t* flags = (int32_t*)w;
     w += slot_flag_bytes(ns);
-    int32_t* pcount = (int32_t*)w;
+    int32_t* cnt = (int32_t*)w;
     w += 256;
     int64_t* pidx = (int64_t*)w;
     w += (size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255;
     int32_t* pready = (int32_t*)w;
     w += slot_flag_bytes(pc);
+    int64_t* ovf = (int64_t*)w;
+    w += ovf_bytes(P, B);
     void* slots = w;
     w += (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns;
     void* park = w;
-    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, park counters)
+    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, counters)
     if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
     if (e != hipSuccess) return e;
-    const WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
-                     (int32_t)ns, (int32_t)slot_elems(P), pcount, (int32_t)pc, pidx, pready, pcount + 1, pcount + 2,
-                     park, (int64_t)park_elems(P)};
+    WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
+               (int32_t)ns, (int32_t)slot_elems(P), cnt, (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
+               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0};
     void* args[] = {(void*)&a};
     const void* rf = resume_kernel(P);
     e = hipFuncGetAttributes(&fa, rf);
@@ -221,7 +245,9 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     // fork: the resume workers on the aux stream alongside the batch kernel; join: the
-    // stream continues after both (no host synchronisation; graph-capturable)
+    // stream continues after both (no host synchronisation).  Under graph capture the two
+    // branches need not run concurrently: the workers then exit at once (take_parked) and
+    // the drain takes every parked problem.
     const bool fork = aux && aux != stream && ev_fork && ev_join;
     if (fork) {
         e = hipEventRecord(ev_fork, stream);
@@ -243,6 +269,13 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fork) {
         e = hipEventRecord(ev_join, aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
+        if (e != hipSuccess) return e;
+    }
+    // the park-area overflow (only where it can occur: pc < B), after every worker that
+    // holds a park entry: problems solved again from the start, one per park entry at a time
+    if (pc < B) {
+        a.phase = 1;
+        e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();

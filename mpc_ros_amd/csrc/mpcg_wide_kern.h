@@ -29,10 +29,10 @@ struct WideArgs {
     int32_t* status;
     double* obj;
     int32_t* iters;
-    int32_t* diag;         // [B][4] restoration phases, filter overflows, parked, 0 (or null)
+    int32_t* diag;         // [B][4] restoration phases, filter overflows, parked (1) / re-solved (2), filter peak (or null)
     void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
     int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
-    int32_t nslots;        // kXcds partitions of nslots / kXcds slots, one per XCD
+    int32_t nslots;        // nxcc partitions of nslots / nxcc slots, one per XCD
     int32_t slot_elems;    // WideLayout::spill() rounded up to whole 128-byte lines
     // parked problems (the restoration phase, continued by k_resume_wide while the batch
     // kernel runs): count, capacity, problem index, ready flag and state of each; the entries
@@ -45,6 +45,14 @@ struct WideArgs {
     int32_t* done;
     void* park;
     int64_t park_stride;   // elements of T per park entry (WideSolver::park_elems, whole 128-byte lines)
+    int32_t* started;      // set by the batch kernel's first workgroup (the resume workers' liveness test)
+    // problems that needed the restoration phase while the park area was full: their indices,
+    // solved again from the start by the overflow launch (phase 1 of k_resume_wide)
+    int32_t* ovf_count;
+    int32_t* ovf_taken;
+    int64_t* ovf_idx;
+    int32_t nxcc;          // XCDs of the device (hipDeviceAttributeNumberOfXccs): slot partitions
+    int32_t phase;         // k_resume_wide: 0 parked problems, 1 park-area overflow
 };
 // the wavefront's end in k_solve_wide (after its results / its parked state are written).
 // No fence: the count only tells the resume workers when every workgroup has finished, and
@@ -54,27 +62,29 @@ __device__ __forceinline__ void block_done(int32_t* done) {
     if (threadIdx.x == 0) atomicAdd(done, 1);
 }
 
-// The XCD the wavefront runs on (HW_REG_XCC_ID, 0..7 on MI355X).
-constexpr int kXcds = 8;
-__device__ __forceinline__ int xcc_id() {
+constexpr int kXcds = 8;  // (MI355X; the runtime's count is used where it can say: device_xccs)
+// The XCD the wavefront runs on (HW_REG_XCC_ID; 0..7 on MI355X in SPX mode), reduced to the
+// device's nxcc XCDs (a partitioned device reports fewer)
+__device__ __forceinline__ int xcc_id(int nxcc) {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return (int)(v & 15) % kXcds;
+    return (int)(v & 15) % nxcc;
 }
 
 // A workspace slot for the wavefront's problem, from the partition of the XCD it runs on:
 // the first free one from blockIdx on (a partition holds 4x the wavefronts an XCD keeps
 // resident, so the first probe normally succeeds; with fewer, a wavefront waits for a
 // resident one on its XCD to finish and release its slot).  A slot is therefore only ever
-// touched through one XCD's L2, and every owner writes a slot location before it reads it
-// (the watchdog, acceptable-point, SOC and soft-restoration copies, the filter's workspace
-// entries): no data crosses wavefronts, so claim and release need no acquire / release
-// fence (an agent-scope release is a write-back of the whole XCD L2, buffer_wbl2, per
-// wavefront: 1.6 GB of write traffic per B = 65,536 launch when it was there).  Slot
-// lines are whole 128-byte lines, so two XCDs never share one.  Vector atomics (device
-// scope) on the flags.
-__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int64_t hint) {
-    const int per = nslots / kXcds, base = xcc_id() * per;
+// touched through one XCD's L2, so handing it over needs no agent-scope fence (an agent
+// release is a write-back of the whole XCD L2, buffer_wbl2, per wavefront: 1.6 GB of write
+// traffic per B = 65,536 launch when it was there).  The hand-over is ordered within the
+// XCD: release_slot waits for the owner's stores to complete (they are in the XCD's L2
+// then; the vector L1 is write-through) before the flag is cleared, and claim_slot
+// invalidates the claiming CU's vector L1 after the flag is taken, so no line a previous
+// owner wrote through another CU is read stale.  Slot lines are whole 128-byte lines, so two
+// XCDs never share one.  Vector atomics (device scope) on the flags.
+__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int nxcc, int64_t hint) {
+    const int per = nslots / nxcc, base = xcc_id(nxcc) * per;
     int s = (int)(hint % per);
     int r = 0;
     if (threadIdx.x == 0) {
@@ -85,9 +95,12 @@ __device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int64_t hi
         }
         r = base + s;
     }
-    return __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+    r = __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");  // (acquire: the CU's L1)
+    return r;
 }
 __device__ __forceinline__ void release_slot(int32_t* flags, int s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (release: the slot's stores are in L2)
     __builtin_amdgcn_wave_barrier();
     if (threadIdx.x == 0) atomicExch(&flags[s], 0);
 }
@@ -122,7 +135,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     wv.t = t;
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
-    const int slot = claim_slot(a.slot_flags, a.nslots, (int64_t)blockIdx.x);
+    if (blockIdx.x == 0 && t == 0) atomicExch(a.started, 1);
+    const int slot = claim_slot(a.slot_flags, a.nslots, a.nxcc, (int64_t)blockIdx.x);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     S.solve();
@@ -142,7 +156,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             block_done(a.done);
             return;
         }
-        S.status = IPM_RESTORATION_FAILURE;  // (more parked problems than the park area holds)
+        // the park area is full: the problem is solved again from the start by the overflow
+        // launch after the drain (the same iterates; its outputs are written there)
+        int o = 0;
+        if (t == 0) {
+            o = atomicAdd(a.ovf_count, 1);
+            a.ovf_idx[o] = p;
+        }
+        release_slot(a.slot_flags, slot);
+        block_done(a.done);
+        return;
     }
     write_out(a, S, p, 0);
     release_slot(a.slot_flags, slot);
@@ -185,11 +208,15 @@ __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t 
 // alongside the batch kernel: a few workers take parked problems as they appear (a problem
 // that parks early in the batch is resumed while the batch still runs) and exit once every
 // workgroup of the batch kernel has finished and every parked problem is taken.  A worker
-// that sees no progress of the batch kernel for 20 s exits (the batch kernel failed).
+// exits early when the batch kernel has not started within ~2 ms (the two launches do not
+// run concurrently, e.g. a graph executor that orders the fork's branches: the drain launch
+// after the batch kernel takes every parked problem then), and when the batch kernel makes
+// no progress for 20 s (it failed).
 __device__ __forceinline__ int take_parked(const WideArgs& a) {
     int r = -1;
     if (threadIdx.x == 0) {
-        uint64_t t0 = wall_clock64();
+        const uint64_t t_start = wall_clock64();
+        uint64_t t0 = t_start;
         int last_done = -1;
         for (;;) {
             const int d = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -205,10 +232,14 @@ __device__ __forceinline__ int take_parked(const WideArgs& a) {
             }
             // (a workgroup parks before it counts itself done: all parked once done == B)
             if ((int64_t)d >= a.B && tk >= c) break;
+            const uint64_t now = wall_clock64();
+            if (d == 0 && now - t_start > (uint64_t)200000 &&  // 2 ms at 100 MHz
+                __hip_atomic_load(a.started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                break;
             if (d != last_done) {
                 last_done = d;
-                t0 = wall_clock64();
-            } else if (wall_clock64() - t0 > (uint64_t)2000000000) {  // 20 s at 100 MHz
+                t0 = now;
+            } else if (now - t0 > (uint64_t)2000000000) {  // 20 s at 100 MHz
                 break;
             }
             __builtin_amdgcn_s_sleep(32);
@@ -222,6 +253,18 @@ __device__ __forceinline__ int take_parked(const WideArgs& a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return r;
 }
+// phase 1: the next problem of the park-area overflow list (the list is complete: the launch
+// follows the batch kernel and the drain in stream order), -1 when none is left
+__device__ __forceinline__ int64_t take_overflow(const WideArgs& a) {
+    int64_t p = -1;
+    if (threadIdx.x == 0) {
+        const int o = atomicAdd(a.ovf_taken, 1);
+        if (o < __hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) p = a.ovf_idx[o];
+    }
+    const int lo = __builtin_amdgcn_readfirstlane(__shfl((int)(p & 0xffffffff), 0, 64));
+    const int hi = __builtin_amdgcn_readfirstlane(__shfl((int)(p >> 32), 0, 64));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
 
 // (one wavefront per SIMD: the restoration phase and the resumed solve get the whole
 // register file -- the workers are few, and the drain runs after the batch kernel)
@@ -231,9 +274,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     const WideLayout Lw(a.P.N, a.P.filter_cap, MODEL);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     for (;;) {
-        const int e = take_parked(a);
-        if (e < 0) return;
-        const int64_t p = a.park_idx[e];
+        int64_t p;
+        T* ent;
+        if (a.phase == 0) {
+            const int e = take_parked(a);
+            if (e < 0) return;
+            p = a.park_idx[e];
+            ent = (T*)a.park + (int64_t)e * a.park_stride;
+        } else {
+            // the whole solve, in park entry blockIdx.x's workspace (the drain has finished)
+            p = take_overflow(a);
+            if (p < 0) return;
+            ent = (T*)a.park + (int64_t)blockIdx.x * a.park_stride;
+        }
         IpmProblem<T> pr;
 #pragma unroll
         for (int j = 0; j < 6; ++j) pr.init[j] = (T)a.state[p * 6 + j];
@@ -241,11 +294,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         for (int j = 0; j < 4; ++j) pr.c[j] = (T)a.coeffs[p * 4 + j];
         DevWave wv;
         wv.t = t;
-        T* ent = (T*)a.park + (int64_t)e * a.park_stride;
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
-        S.unpark(ent);
+        if (a.phase == 0)
+            S.unpark(ent);
+        else
+            S.solve();
         S.finish_resto();
-        write_out(a, S, p, 1);
+        write_out(a, S, p, a.phase == 0 ? 1 : 2);
     }
 }
 
@@ -253,6 +308,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 // k_solve_wide<MODEL, SPLIT, T, NB, DEFOPT, WPE> / k_resume_wide<MODEL, SPLIT, T, NB>.
 template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT, int WPE>
 const void* solve_kernel_fn();
+// (the dispatcher's choice: the instance and its name, "k_solve_wide<M,S,T,NB,D,W>")
+struct WideInst {
+    const void* fn;
+    const char* name;
+};
+WideInst wide_kernel(const IpmParams& P, int64_t B);
+int device_xccs();
 template <int MODEL, bool SPLIT, class T, int NB>
 const void* resume_kernel_fn();
 

@@ -75,6 +75,15 @@ class BatchSolver:
         self.params = p
         self.N = p.steps
 
+    def set_park_capacity(self, cap: int = 0):
+        """Park-area entries (0: the default max(256, B / 128)); results do not depend on it."""
+        _lib.check(_lib.lib().mpcg_set_park_capacity(self._h, int(cap)), "mpcg_set_park_capacity")
+
+    @property
+    def last_kernel(self) -> str:
+        """The solver kernel instance the last solve launched ("k_solve_wide<...>")."""
+        return _lib.lib().mpcg_last_kernel(self._h).decode()
+
     def reserve(self, B: int):
         _lib.check(_lib.lib().mpcg_reserve(self._h, int(B)), "mpcg_reserve")
 
