@@ -63,8 +63,8 @@ def algorithmic_flops_per_solve(N: int, iters_mean: float) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=80, help="timed steps (default: a timed region of ~1.3 s)")
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536, help="problems per GPU")
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--gather-traj", action="store_true", help="also gather the 3N trajectories")
@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--selftest", action="store_true",
                     help="launch/shard/gather plumbing only: gloo on CPU, a stub solver that writes each "
                          "problem's global index (tests/test_bench_launch.py); no GPU, no timing claim")
+    ap.add_argument("--restoration", default="auto", choices=["auto", "on", "off"],
+                    help="Ipopt's feasibility-restoration phase: auto = the dtype's default (fp64 on; the fp32 "
+                         "solver's FP32_OPTIONS off), on / off = mpcg_params.no_restoration 0 / 1")
     ap.add_argument("--mode", default="solve", choices=["solve", "track"],
                     help="solve: MPC::Solve on preprocessed inputs (the metric); track: the whole control "
                          "tick from raw poses and waypoint plans (findBestPath + solve + post-processing)")
@@ -297,7 +300,8 @@ def main():
         tvel = torch.from_numpy(np.ascontiguousarray(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))).to(dev)
         tplan = torch.from_numpy(np.ascontiguousarray(plan)).to(dev)
         cmd = torch.empty((count, 3), dtype=torch.float64, device=dev)
-    solver = BatchSolver(dev.index, P, strategy=a.strategy, dtype=a.dtype)
+    extra = {} if a.restoration == "auto" else {"no_restoration": int(a.restoration == "off")}
+    solver = BatchSolver(dev.index, P, strategy=a.strategy, dtype=a.dtype, **extra)
     solver.reserve(count)
     u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
     traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)
@@ -411,10 +415,10 @@ def main():
                                    f"(MPC::Solve NLP, Ipopt algorithm), N={N}, {a.dtype}, "
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",
                        "batch_per_gpu": B, "total_batch": total, "horizon": N, "parallelism": f"dp{world}",
-                       "mode": a.mode, "model": a.model, "dtype": a.dtype},
+                       "mode": a.mode, "model": a.model, "dtype": a.dtype, "restoration": a.restoration},
             "roofline": {"bound": "valu_fp64" if a.dtype == "fp64" else "valu_fp32", "achieved": got_a,
                          "peak": peak_a, "unit": "TFLOP/s", "frac": got_a / peak_a, "traffic": traffic,
-                         "kernel": "mpcg::k_solve_wide", "kernel_ms": kern,
+                         "kernel": solver.last_kernel, "kernel_ms": kern,
                          "algorithmic_flops_per_solve": af, "solves_per_launch": count,
                          "traffic_source": f"profiles/{prof}.json" if traffic else None,
                          "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

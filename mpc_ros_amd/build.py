@@ -75,7 +75,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     # the backend would otherwise move a private array into static LDS, which the launch
     # refuses -- mpcg_wide.hip checks sharedSizeBytes == 0)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-             "-mllvm", "-disable-promote-alloca-to-lds",
+             "-mllvm", "-disable-promote-alloca-to-lds", "-mllvm", "-disable-machine-licm",
              "-Wno-unused-result", "-Wno-unused-value",
              f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"',
              "-Rpass-analysis=kernel-resource-usage"]
