@@ -188,14 +188,25 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
                          double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, int32_t* d_diag,
                          void* stream);
 
-/* Multi-GPU batched solve from one process, host buffers as
+/* Multi-GPU batched solves from one process, host buffers as
  * mpcg_solve: the B problems are split into ngpu contiguous shards (the first B % ngpu
  * GPUs take one more), solved on devices[r] with the given parameters, and the results are
  * gathered to devices[0] by grouped RCCL send/recv (one message per output array and GPU,
- * point-to-point over xGMI), then copied to the host.  Creates and destroys its handles and
- * communicator per call (a serving loop keeps per-GPU handles and gathers itself, as
- * bench.py does with torch.distributed).  Returns 0, or < 0 with mpcg_last_error() set
- * (-1 arguments, -2 HIP, -3 device ordinal, -4 RCCL). */
+ * point-to-point over xGMI), then copied to the host.
+ *
+ * mpcg_multi: a persistent context for a serving loop -- the RCCL communicator
+ * (ncclCommInitAll), a handle, stream and device buffers per GPU, and each handle's solver
+ * workspace reserved for the largest shard of B_max problems, all created once by
+ * mpcg_multi_create; mpcg_multi_solve then allocates nothing (batches of B <= B_max; the
+ * parameters are the context's).  A failure inside the gather group aborts the communicators
+ * and marks the context broken (later solves return -4; destroy and create it again).
+ * mpcg_solve_multi = create + solve + destroy for one batch.  Returns 0, or < 0 with
+ * mpcg_last_error() set (-1 arguments, -2 HIP, -3 device ordinal, -4 RCCL). */
+typedef struct mpcg_multi mpcg_multi;
+int mpcg_multi_create(int ngpu, const int* devices, const mpcg_params* params, int64_t B_max, mpcg_multi** out);
+int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
+                     int32_t* status, double* obj, int32_t* iters);
+void mpcg_multi_destroy(mpcg_multi* m);
 int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
                      const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters);
 
@@ -214,6 +225,11 @@ typedef struct mpcg_xfer {
 int mpcg_shard_range(int64_t B, int ngpu, int r, int64_t* start, int64_t* count);
 int mpcg_multi_gather_plan(int64_t B, int32_t N, int ngpu, int r, mpcg_xfer* xfers);
 size_t mpcg_multi_out_bytes(int64_t B, int32_t N);
+/* mpcg_multi_buffer_bytes: the device buffers a context for batches of up to B_max holds on
+ * GPU r (inputs of the largest shard; outputs of that shard, or on the root the gathered
+ * outputs of B_max problems), besides the handle's solver workspace (mpcg_workspace_bytes of
+ * the largest shard).  0 for invalid arguments. */
+size_t mpcg_multi_buffer_bytes(int64_t B_max, int32_t N, int ngpu, int r);
 
 /* Tracking::findBestPath's preprocessing (mpc_ros/src/driving_state.cpp:175-256) on the
  * device for B robots: waypoints to the vehicle frame, cubic polyfit (Householder QR),

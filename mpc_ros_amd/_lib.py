@@ -83,6 +83,10 @@ SIGNATURES = {
     "mpcg_shard_range": ([C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
     "mpcg_multi_gather_plan": ([C.c_int64, C.c_int32, C.c_int, C.c_int, C.c_void_p], C.c_int),
     "mpcg_multi_out_bytes": ([C.c_int64, C.c_int32], C.c_size_t),
+    "mpcg_multi_buffer_bytes": ([C.c_int64, C.c_int32, C.c_int, C.c_int], C.c_size_t),
+    "mpcg_multi_create": ([C.c_int, C.POINTER(C.c_int), _PP, C.c_int64, C.POINTER(C.c_void_p)], C.c_int),
+    "mpcg_multi_solve": ([C.c_void_p, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip], C.c_int),
+    "mpcg_multi_destroy": ([C.c_void_p], None),
     "mpcg_set_strategy": ([C.c_void_p, C.c_int32], C.c_int),
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
     "mpcg_set_park_capacity": ([C.c_void_p, C.c_int64], C.c_int),

@@ -1,4 +1,6 @@
-// mpc_ros_amd/csrc/mpcg_multi.cpp -- mpcg_solve_multi: one process, several GPUs, RCCL gather.
+// mpc_ros_amd/csrc/mpcg_multi.cpp -- one process, several GPUs, RCCL gather: the persistent
+// context mpcg_multi (create once, solve many batches, destroy) and mpcg_solve_multi (the
+// same for one batch).
 //
 // the B problems are independent, so they are split into contiguous
 // shards (mpcg_shard_range: the first B % G GPUs take one extra problem), each GPU solves
@@ -6,8 +8,11 @@
 // the first GPU with one grouped RCCL send/recv per output array (mpcg_multi_gather_plan:
 // rank r sends its shard, the root receives every shard at its offset -- point-to-point
 // over xGMI, the north star's "RCCL used only for the final gather"), then copied to the
-// caller's host buffers.  Every HIP and RCCL return is checked; a failure sets
-// mpcg_last_error() and the call drains its streams before it frees anything.
+// caller's host buffers.  The context holds the communicator, a handle, stream and device
+// buffers per GPU, and each handle's solver workspace reserved for the largest shard: a
+// solve allocates nothing.  Every HIP and RCCL return is checked; a failure sets
+// mpcg_last_error(); a failure inside the gather group aborts the communicators (an
+// unmatched send must not be waited for) and marks the context broken.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -82,131 +87,214 @@ size_t mpcg_multi_out_bytes(int64_t B, int32_t N) {
     return B < 0 || N < 1 ? 0 : OutLayout{B, N}.total();
 }
 
-int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
-                     const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters) {
-    if (ngpu < 1 || !devices || !params) return mpcg::set_error(-1, "mpcg_solve_multi: ngpu >= 1, devices, params");
-    if (B < 0) return mpcg::set_error(-1, "mpcg_solve_multi: B < 0");
-    if (B == 0) return 0;
-    if (!state || !coeffs || !u0) return mpcg::set_error(-1, "mpcg_solve_multi: null state / coeffs / u0");
+// the context's device buffers on GPU r for batches of up to B_max: the inputs of its largest
+// shard, and its outputs (the root: the gathered outputs of B_max problems); the solver
+// workspace its handle reserves comes on top (mpcg_workspace_bytes of the largest shard)
+size_t mpcg_multi_buffer_bytes(int64_t B_max, int32_t N, int ngpu, int r) {
+    if (B_max < 0 || N < 1 || ngpu < 1 || r < 0 || r >= ngpu) return 0;
+    int64_t start = 0, count = 0;
+    mpcg_shard_range(B_max, ngpu, 0, &start, &count);  // (GPU 0's shard is a largest one)
+    const size_t in = sizeof(double) * 10 * (size_t)(count > 0 ? count : 1);
+    const size_t out = OutLayout{r == 0 ? B_max : count, N}.total();
+    return in + (out > 0 ? out : 1);
+}
+
+}  // extern "C"
+
+struct mpcg_multi {
+    int ngpu = 0;
+    int N = 0;
+    int64_t B_max = 0;
+    bool broken = false;  // a gather failed inside its group: the communicators were aborted
+    std::vector<Shard> sh;
+    std::vector<ncclComm_t> comms;
+};
+
+namespace {
+// (drains every stream before it frees: a failure may leave work queued; aborted
+// communicators first, so that no stream waits for an unmatched transfer)
+void multi_free(mpcg_multi* m) {
+    if (m->broken)
+        for (auto& c : m->comms)
+            if (c) {
+                ncclCommAbort(c);
+                c = nullptr;
+            }
+    for (auto& s : m->sh) {
+        hipSetDevice(s.dev);
+        if (s.s) hipStreamSynchronize(s.s);
+        if (s.h) mpcg_destroy(s.h);
+        if (s.in) hipFree(s.in);
+        if (s.out) hipFree(s.out);
+        if (s.s) hipStreamDestroy(s.s);
+        s = Shard{};
+    }
+    for (auto c : m->comms)
+        if (c) ncclCommDestroy(c);
+    m->comms.clear();
+}
+}  // namespace
+
+extern "C" {
+
+int mpcg_multi_create(int ngpu, const int* devices, const mpcg_params* params, int64_t B_max, mpcg_multi** out) {
+    if (!out) return mpcg::set_error(-1, "mpcg_multi_create: null out");
+    *out = nullptr;
+    if (ngpu < 1 || !devices || !params) return mpcg::set_error(-1, "mpcg_multi_create: ngpu >= 1, devices, params");
+    if (B_max < 1) return mpcg::set_error(-1, "mpcg_multi_create: B_max >= 1");
     int rc = mpcg_params_check(params);
     if (rc) return rc;
     int ndev = 0;
     hipError_t he = hipGetDeviceCount(&ndev);
     if (he != hipSuccess) return hip_fail(he, "hipGetDeviceCount");
     for (int r = 0; r < ngpu; ++r) {
-        if (devices[r] < 0 || devices[r] >= ndev) return mpcg::set_error(-3, "mpcg_solve_multi: device out of range");
+        if (devices[r] < 0 || devices[r] >= ndev) return mpcg::set_error(-3, "mpcg_multi_create: device out of range");
         for (int q = 0; q < r; ++q)
-            if (devices[q] == devices[r]) return mpcg::set_error(-1, "mpcg_solve_multi: devices repeat");
+            if (devices[q] == devices[r]) return mpcg::set_error(-1, "mpcg_multi_create: devices repeat");
     }
-    const int N = params->steps;
-    std::vector<Shard> sh(ngpu);
-    for (int r = 0; r < ngpu; ++r) {
-        sh[r].dev = devices[r];
-        mpcg_shard_range(B, ngpu, r, &sh[r].start, &sh[r].count);
-    }
-    std::vector<ncclComm_t> comms(ngpu, nullptr);
-    // (drains every stream before it frees: a failure may leave work queued)
-    auto cleanup = [&]() {
-        for (auto& s : sh) {
-            hipSetDevice(s.dev);
-            if (s.s) hipStreamSynchronize(s.s);
-            if (s.h) mpcg_destroy(s.h);
-            if (s.in) hipFree(s.in);
-            if (s.out) hipFree(s.out);
-            if (s.s) hipStreamDestroy(s.s);
-        }
-        for (auto c : comms)
-            if (c) ncclCommDestroy(c);
-    };
+    mpcg_multi* m = new mpcg_multi();
+    m->ngpu = ngpu;
+    m->N = params->steps;
+    m->B_max = B_max;
+    m->sh.resize(ngpu);
+    m->comms.assign(ngpu, nullptr);
+    int64_t start = 0, cmax = 0;
+    mpcg_shard_range(B_max, ngpu, 0, &start, &cmax);
     int result = 0;
     do {
-        ncclResult_t ne = ncclCommInitAll(comms.data(), ngpu, devices);
+        ncclResult_t ne = ncclCommInitAll(m->comms.data(), ngpu, devices);
         if (ne != ncclSuccess) { result = nccl_fail(ne, "ncclCommInitAll"); break; }
-        // shards: copy in, solve (each on its own GPU and stream, queued without waiting)
         for (int r = 0; r < ngpu && !result; ++r) {
-            Shard& s = sh[r];
+            Shard& s = m->sh[r];
+            s.dev = devices[r];
             if ((rc = mpcg_create(s.dev, &s.h)) != 0) { result = rc; break; }
             if ((rc = mpcg_set_params(s.h, params)) != 0) { result = rc; break; }
+            if ((rc = mpcg_reserve(s.h, cmax)) != 0) { result = rc; break; }
             if ((he = hipSetDevice(s.dev)) != hipSuccess) { result = hip_fail(he, "hipSetDevice"); break; }
             if ((he = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking)) != hipSuccess) {
                 result = hip_fail(he, "hipStreamCreateWithFlags");
                 break;
             }
-            const size_t out_bytes = OutLayout{r == 0 ? B : s.count, N}.total();
-            if ((he = hipMalloc((void**)&s.in, sizeof(double) * 10 * (s.count > 0 ? s.count : 1))) != hipSuccess ||
-                (he = hipMalloc((void**)&s.out, out_bytes > 0 ? out_bytes : 1)) != hipSuccess) {
+            const size_t in_bytes = sizeof(double) * 10 * (size_t)(cmax > 0 ? cmax : 1);
+            const size_t out_bytes = mpcg_multi_buffer_bytes(B_max, m->N, ngpu, r) - in_bytes;
+            if ((he = hipMalloc((void**)&s.in, in_bytes)) != hipSuccess ||
+                (he = hipMalloc((void**)&s.out, out_bytes)) != hipSuccess) {
                 result = hip_fail(he, "hipMalloc");
-                break;
-            }
-            if (s.count == 0) continue;
-            double* din = s.in;
-            if ((he = hipMemcpyAsync(din, state + 6 * s.start, sizeof(double) * 6 * s.count, hipMemcpyHostToDevice,
-                                     s.s)) != hipSuccess ||
-                (he = hipMemcpyAsync(din + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count,
-                                     hipMemcpyHostToDevice, s.s)) != hipSuccess) {
-                result = hip_fail(he, "hipMemcpyAsync (inputs)");
-                break;
-            }
-            // the root solves into its own slot of the gathered arrays (the plan's src offsets)
-            mpcg_xfer x[MPCG_GATHER_ARRAYS];
-            if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) { result = rc; break; }
-            char* o = s.out;
-            rc = mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + x[0].src_offset),
-                                   (double*)(o + x[1].src_offset), (int32_t*)(o + x[3].src_offset),
-                                   (double*)(o + x[2].src_offset), (int32_t*)(o + x[4].src_offset), s.s);
-            if (rc) { result = rc; break; }
-        }
-        if (result) break;
-        // the gather: rank r > 0 sends each of its output arrays, the root receives them at
-        // their offsets (grouped point-to-point: every shard moves once over xGMI).  Within
-        // the group the first failing call is kept and the group is still closed.
-        if ((ne = ncclGroupStart()) != ncclSuccess) { result = nccl_fail(ne, "ncclGroupStart"); break; }
-        int grc = 0;
-        for (int r = 1; r < ngpu && !grc; ++r) {
-            const Shard& s = sh[r];
-            if (s.count == 0) continue;
-            mpcg_xfer x[MPCG_GATHER_ARRAYS];
-            if ((grc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) break;
-            for (const auto& p : x) {
-                if ((ne = ncclSend(s.out + p.src_offset, p.bytes, ncclChar, 0, comms[r], s.s)) != ncclSuccess) {
-                    grc = nccl_fail(ne, "ncclSend");
-                    break;
-                }
-                if ((ne = ncclRecv(sh[0].out + p.dst_offset, p.bytes, ncclChar, r, comms[0], sh[0].s)) != ncclSuccess) {
-                    grc = nccl_fail(ne, "ncclRecv");
-                    break;
-                }
-            }
-        }
-        ne = ncclGroupEnd();
-        if (grc) { result = grc; break; }
-        if (ne != ncclSuccess) { result = nccl_fail(ne, "ncclGroupEnd"); break; }
-        // results to the host from the root
-        if ((he = hipSetDevice(sh[0].dev)) != hipSuccess) { result = hip_fail(he, "hipSetDevice"); break; }
-        const OutLayout G{B, N};
-        const char* o = sh[0].out;
-        hipStream_t s0 = sh[0].s;
-        struct { void* host; size_t off, bytes; } back[MPCG_GATHER_ARRAYS] = {
-            {u0, G.u0(), sizeof(double) * 2 * B}, {traj, G.traj(), sizeof(double) * 3 * N * B},
-            {obj, G.obj(), sizeof(double) * B}, {status, G.status(), sizeof(int32_t) * B},
-            {iters, G.iters(), sizeof(int32_t) * B}};
-        for (const auto& b : back) {
-            if (!b.host) continue;
-            if ((he = hipMemcpyAsync(b.host, o + b.off, b.bytes, hipMemcpyDeviceToHost, s0)) != hipSuccess) {
-                result = hip_fail(he, "hipMemcpyAsync (results)");
-                break;
-            }
-        }
-        if (result) break;
-        for (auto& s : sh) {
-            if ((he = hipSetDevice(s.dev)) != hipSuccess || (he = hipStreamSynchronize(s.s)) != hipSuccess) {
-                result = hip_fail(he, "hipStreamSynchronize");
                 break;
             }
         }
     } while (false);
-    cleanup();
-    return result;
+    if (result) {
+        multi_free(m);
+        delete m;
+        return result;
+    }
+    *out = m;
+    return 0;
+}
+
+void mpcg_multi_destroy(mpcg_multi* m) {
+    if (!m) return;
+    multi_free(m);
+    delete m;
+}
+
+int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
+                     int32_t* status, double* obj, int32_t* iters) {
+    if (!m) return mpcg::set_error(-1, "mpcg_multi_solve: null context");
+    if (m->broken) return mpcg::set_error(-4, "mpcg_multi_solve: the context's communicators were aborted");
+    if (B < 0 || B > m->B_max) return mpcg::set_error(-1, "mpcg_multi_solve: 0 <= B <= the context's B_max");
+    if (B == 0) return 0;
+    if (!state || !coeffs || !u0) return mpcg::set_error(-1, "mpcg_multi_solve: null state / coeffs / u0");
+    const int ngpu = m->ngpu, N = m->N;
+    std::vector<Shard>& sh = m->sh;
+    for (int r = 0; r < ngpu; ++r) mpcg_shard_range(B, ngpu, r, &sh[r].start, &sh[r].count);
+    hipError_t he;
+    int rc;
+    // shards: copy in, solve (each on its own GPU and stream, queued without waiting)
+    for (int r = 0; r < ngpu; ++r) {
+        Shard& s = sh[r];
+        if (s.count == 0) continue;
+        if ((he = hipSetDevice(s.dev)) != hipSuccess) return hip_fail(he, "hipSetDevice");
+        double* din = s.in;
+        if ((he = hipMemcpyAsync(din, state + 6 * s.start, sizeof(double) * 6 * s.count, hipMemcpyHostToDevice,
+                                 s.s)) != hipSuccess ||
+            (he = hipMemcpyAsync(din + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count,
+                                 hipMemcpyHostToDevice, s.s)) != hipSuccess)
+            return hip_fail(he, "hipMemcpyAsync (inputs)");
+        // the root solves into its own slot of the gathered arrays (the plan's src offsets)
+        mpcg_xfer x[MPCG_GATHER_ARRAYS];
+        if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) return rc;
+        char* o = s.out;
+        rc = mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + x[0].src_offset),
+                               (double*)(o + x[1].src_offset), (int32_t*)(o + x[3].src_offset),
+                               (double*)(o + x[2].src_offset), (int32_t*)(o + x[4].src_offset), s.s);
+        if (rc) return rc;
+    }
+    // the gather: rank r > 0 sends each of its output arrays, the root receives them at their
+    // offsets (grouped point-to-point: every shard moves once over xGMI).  The plan is checked
+    // before the group opens; a failing call inside it aborts the communicators (ncclGroupEnd
+    // would otherwise launch an unmatched send that a stream then waits for).
+    std::vector<mpcg_xfer> plan((size_t)ngpu * MPCG_GATHER_ARRAYS);
+    for (int r = 1; r < ngpu; ++r)
+        if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, &plan[(size_t)r * MPCG_GATHER_ARRAYS])) != 0) return rc;
+    ncclResult_t ne = ncclGroupStart();
+    if (ne != ncclSuccess) return nccl_fail(ne, "ncclGroupStart");
+    int grc = 0;
+    for (int r = 1; r < ngpu && !grc; ++r) {
+        const Shard& s = sh[r];
+        if (s.count == 0) continue;
+        for (int k = 0; k < MPCG_GATHER_ARRAYS && !grc; ++k) {
+            const mpcg_xfer& p = plan[(size_t)r * MPCG_GATHER_ARRAYS + k];
+            if ((ne = ncclSend(s.out + p.src_offset, p.bytes, ncclChar, 0, m->comms[r], s.s)) != ncclSuccess)
+                grc = nccl_fail(ne, "ncclSend");
+            else if ((ne = ncclRecv(sh[0].out + p.dst_offset, p.bytes, ncclChar, r, m->comms[0], sh[0].s)) != ncclSuccess)
+                grc = nccl_fail(ne, "ncclRecv");
+        }
+    }
+    if (grc) {
+        m->broken = true;
+        for (auto& c : m->comms) ncclCommAbort(c), c = nullptr;
+        ncclGroupEnd();
+        return grc;
+    }
+    if ((ne = ncclGroupEnd()) != ncclSuccess) {
+        m->broken = true;
+        for (auto& c : m->comms) ncclCommAbort(c), c = nullptr;
+        return nccl_fail(ne, "ncclGroupEnd");
+    }
+    // results to the host from the root
+    if ((he = hipSetDevice(sh[0].dev)) != hipSuccess) return hip_fail(he, "hipSetDevice");
+    const OutLayout G{B, N};
+    const char* o = sh[0].out;
+    hipStream_t s0 = sh[0].s;
+    struct { void* host; size_t off, bytes; } back[MPCG_GATHER_ARRAYS] = {
+        {u0, G.u0(), sizeof(double) * 2 * B}, {traj, G.traj(), sizeof(double) * 3 * N * B},
+        {obj, G.obj(), sizeof(double) * B}, {status, G.status(), sizeof(int32_t) * B},
+        {iters, G.iters(), sizeof(int32_t) * B}};
+    for (const auto& b : back) {
+        if (!b.host) continue;
+        if ((he = hipMemcpyAsync(b.host, o + b.off, b.bytes, hipMemcpyDeviceToHost, s0)) != hipSuccess)
+            return hip_fail(he, "hipMemcpyAsync (results)");
+    }
+    for (auto& s : sh)
+        if ((he = hipSetDevice(s.dev)) != hipSuccess || (he = hipStreamSynchronize(s.s)) != hipSuccess)
+            return hip_fail(he, "hipStreamSynchronize");
+    return 0;
+}
+
+int mpcg_solve_multi(int ngpu, const int* devices, const mpcg_params* params, int64_t B, const double* state,
+                     const double* coeffs, double* u0, double* traj, int32_t* status, double* obj, int32_t* iters) {
+    if (ngpu < 1 || !devices || !params) return mpcg::set_error(-1, "mpcg_solve_multi: ngpu >= 1, devices, params");
+    if (B < 0) return mpcg::set_error(-1, "mpcg_solve_multi: B < 0");
+    if (B == 0) return 0;
+    if (!state || !coeffs || !u0) return mpcg::set_error(-1, "mpcg_solve_multi: null state / coeffs / u0");
+    mpcg_multi* m = nullptr;
+    int rc = mpcg_multi_create(ngpu, devices, params, B, &m);
+    if (rc) return rc;
+    rc = mpcg_multi_solve(m, B, state, coeffs, u0, traj, status, obj, iters);
+    mpcg_multi_destroy(m);
+    return rc;
 }
 
 }  // extern "C"

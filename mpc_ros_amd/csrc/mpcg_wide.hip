@@ -74,14 +74,25 @@ static const void* rk() {
         return resume_kernel_fn<M, S, T, NB>();
 }
 
+// The fp32 solver does not run the restoration phase itself: a float iterate's line search
+// fails at its noise floor, where a float restoration phase rarely succeeds.  A problem that
+// would enter it is solved again from the start by the fp64 solver with the reference's Ipopt
+// options (mpcg_params.no_restoration = 0, the default; 1 stops it with status 9 instead).
+static bool escalates(const IpmParams& P) { return P.precision == 1 && !P.no_resto; }
+static IpmParams fp64_params(const IpmParams& P) {
+    IpmParams q = P;
+    q.precision = 0;
+    ipopt_default_options(q);
+    return q;
+}
+
 // the resume kernel of a solve kernel's instance (the general-options instance also for the
-// default-options one: the two compute bitwise the same)
+// default-options one: the two compute bitwise the same); for the fp32 solver the fp64
+// instance of the same horizon (its escalations)
 static const void* resume_kernel(const IpmParams& P) {
     const bool split = P.N <= 32;
-    const bool f32 = P.precision == 1;
     const int nb = P.N > 64 ? 2 : 1;
-    if (P.N > 128 || (f32 && P.model != 0)) return nullptr;
-    if (f32) return nb == 2 ? rk<0, false, float, 2>() : split ? rk<0, true, float, 1>() : rk<0, false, float, 1>();
+    if (P.N > 128 || (P.precision == 1 && P.model != 0)) return nullptr;
     if (P.model == 1)
         return nb == 2 ? rk<1, false, double, 2>() : split ? rk<1, true, double, 1>() : rk<1, false, double, 1>();
     return nb == 2 ? rk<0, false, double, 2>() : split ? rk<0, true, double, 1>() : rk<0, false, double, 1>();
@@ -168,9 +179,15 @@ int64_t wide_park_cap(const IpmParams& P, int64_t B) {
     if (P.park_cap > 0) c = P.park_cap;
     return c < B ? c : B;
 }
-// the overflow list: one index per problem (only where the park area can overflow)
+// the overflow list: one index per problem (only where the park area can overflow, and for
+// the fp32 solver's escalations)
 static size_t ovf_bytes(const IpmParams& P, int64_t B) {
-    return wide_park_cap(P, B) < B ? ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255 : 0;
+    return wide_park_cap(P, B) < B || escalates(P) ? ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255 : 0;
+}
+static size_t park_elems(const IpmParams& P);
+// bytes of a park entry (the fp32 solver's escalations: an fp64 problem's)
+static size_t park_entry_bytes(const IpmParams& P) {
+    return escalates(P) ? park_elems(fp64_params(P)) * sizeof(double) : park_elems(P) * elem_bytes(P);
 }
 static size_t park_elems(const IpmParams& P) {
     const WideLayout L(P.N, P.filter_cap, P.model);
@@ -180,8 +197,7 @@ static size_t park_elems(const IpmParams& P) {
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) + slot_flag_bytes(pc) +
-           ovf_bytes(P, B) + (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns +
-           park_elems(P) * elem_bytes(P) * (size_t)pc;
+           ovf_bytes(P, B) + (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns + park_entry_bytes(P) * (size_t)pc;
 }
 
 // Concurrent resume workers (parked problems in flight while the batch kernel runs): each
@@ -233,22 +249,38 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     void* park = w;
     e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, counters)
     if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
+    if (e == hipSuccess && ovf_bytes(P, B)) e = hipMemsetAsync(ovf, 0xFF, ovf_bytes(P, B), stream);  // (all -1)
     if (e != hipSuccess) return e;
+    const bool esc = escalates(P);
+    // (the fp32 solver's batch parks nothing: every problem that needs the restoration phase
+    // goes to the overflow list)
     WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
-               (int32_t)ns, (int32_t)slot_elems(P), cnt, (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
-               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0};
+               (int32_t)ns, (int32_t)slot_elems(P), cnt, esc ? 0 : (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
+               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0, 0, 2};
     void* args[] = {(void*)&a};
+    // the resume workers' arguments: the fp32 solver's escalations run the fp64 solver
+    const IpmParams Pr = esc ? fp64_params(P) : P;
+    WideArgs ar = a;
+    ar.P = Pr;
+    ar.park_stride = (int64_t)park_elems(Pr);
+    if (esc) {
+        ar.phase = 1;
+        ar.ovf_mark = 3;
+    }
+    void* rargs[] = {(void*)&ar};
+    const size_t rlds = wide_lds_bytes(Pr);
     const void* rf = resume_kernel(P);
     e = hipFuncGetAttributes(&fa, rf);
     if (e != hipSuccess) return e;
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
-    e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
     if (e != hipSuccess) return e;
     // fork: the resume workers on the aux stream alongside the batch kernel; join: the
     // stream continues after both (no host synchronisation).  Under graph capture the two
     // branches need not run concurrently: the workers then exit at once (take_parked) and
     // the drain takes every parked problem.
     const bool fork = aux && aux != stream && ev_fork && ev_join;
+    const unsigned workers = fork ? (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B)) : 0u;
     if (fork) {
         e = hipEventRecord(ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);
@@ -256,16 +288,22 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     }
     e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
-    if (fork) {  // the concurrent workers
-        const unsigned workers = (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B));
-        e = hipLaunchKernel(rf, dim3(workers), dim3(64), args, lds, aux);
+    if (fork) {  // the concurrent workers (park entries 0 .. workers - 1 for escalations)
+        e = hipLaunchKernel(rf, dim3(workers), dim3(64), rargs, rlds, aux);
         if (e != hipSuccess) return e;
     }
-    // the drain, after the batch kernel: one worker per park entry, so the problems still
-    // parked when the batch ends run side by side (a worker finding nothing left exits at
-    // once) -- the tail is the longest restoration, not their sum over a few workers
-    e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
-    if (e != hipSuccess) return e;
+    // the drain, after the batch kernel: one worker per park entry (escalations: per park
+    // entry the concurrent workers do not hold), so the problems still waiting when the batch
+    // ends run side by side (a worker finding nothing left exits at once) -- the tail is the
+    // longest restoration, not their sum over a few workers
+    WideArgs ad = ar;
+    ad.ent0 = esc ? (int32_t)workers : 0;
+    void* dargs[] = {(void*)&ad};
+    const unsigned drain = (unsigned)(esc ? pc - workers : pc);
+    if (drain > 0) {
+        e = hipLaunchKernel(rf, dim3(drain), dim3(64), dargs, rlds, stream);
+        if (e != hipSuccess) return e;
+    }
     if (fork) {
         e = hipEventRecord(ev_join, aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
@@ -273,9 +311,12 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     }
     // the park-area overflow (only where it can occur: pc < B), after every worker that
     // holds a park entry: problems solved again from the start, one per park entry at a time
-    if (pc < B) {
-        a.phase = 1;
-        e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, lds, stream);
+    if (!esc && pc < B) {
+        WideArgs ao = ar;
+        ao.phase = 1;
+        ao.ent0 = 0;
+        void* oargs[] = {(void*)&ao};
+        e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), oargs, rlds, stream);
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();

@@ -52,7 +52,12 @@ struct WideArgs {
     int32_t* ovf_taken;
     int64_t* ovf_idx;
     int32_t nxcc;          // XCDs of the device (hipDeviceAttributeNumberOfXccs): slot partitions
-    int32_t phase;         // k_resume_wide: 0 parked problems, 1 park-area overflow
+    // k_resume_wide: 0 parked problems; 1 the overflow list (solved from the start, in park
+    // entry ent0 + blockIdx.x; diag[:, 2] = ovf_mark: 2 park-area overflow, 3 an fp32 problem
+    // solved again in fp64 where the fp32 solver would enter the restoration phase)
+    int32_t phase;
+    int32_t ent0;
+    int32_t ovf_mark;
 };
 // the wavefront's end in k_solve_wide (after its results / its parked state are written).
 // No fence: the count only tells the resume workers when every workgroup has finished, and
@@ -158,10 +163,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         }
         // the park area is full: the problem is solved again from the start by the overflow
         // launch after the drain (the same iterates; its outputs are written there)
-        int o = 0;
+        // (the index is published by an atomic store: a worker on another XCD may take the
+        // entry while the batch runs -- the list starts as -1, written by the launch)
         if (t == 0) {
-            o = atomicAdd(a.ovf_count, 1);
-            a.ovf_idx[o] = p;
+            const int o = atomicAdd(a.ovf_count, 1);
+            atomicExch((unsigned long long*)&a.ovf_idx[o], (unsigned long long)p);
         }
         release_slot(a.slot_flags, slot);
         block_done(a.done);
@@ -253,13 +259,51 @@ __device__ __forceinline__ int take_parked(const WideArgs& a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return r;
 }
-// phase 1: the next problem of the park-area overflow list (the list is complete: the launch
-// follows the batch kernel and the drain in stream order), -1 when none is left
+// phase 1: the next problem of the overflow list, -1 when none is left.  The list may still
+// grow while the batch kernel runs (the fp32 solver's escalations are taken concurrently): an
+// entry is taken by a CAS on the taken count, its index awaited until the batch kernel has
+// published it; the worker exits once every workgroup of the batch has finished and every
+// entry is taken (or, as take_parked, when the batch kernel has not started within ~2 ms or
+// makes no progress for 20 s).
 __device__ __forceinline__ int64_t take_overflow(const WideArgs& a) {
     int64_t p = -1;
     if (threadIdx.x == 0) {
-        const int o = atomicAdd(a.ovf_taken, 1);
-        if (o < __hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) p = a.ovf_idx[o];
+        const uint64_t t_start = wall_clock64();
+        uint64_t t0 = t_start;
+        int last_done = -1;
+        int o = -1;
+        for (;;) {
+            const int d = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const int c = __hip_atomic_load(a.ovf_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const int tk = __hip_atomic_load(a.ovf_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk < c) {
+                if (atomicCAS(a.ovf_taken, tk, tk + 1) == tk) {
+                    o = tk;
+                    break;
+                }
+                continue;
+            }
+            if ((int64_t)d >= a.B) break;  // (a workgroup lists itself before it counts itself done)
+            const uint64_t now = wall_clock64();
+            if (d == 0 && now - t_start > (uint64_t)200000 &&
+                __hip_atomic_load(a.started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                break;
+            if (d != last_done) {
+                last_done = d;
+                t0 = now;
+            } else if (now - t0 > (uint64_t)2000000000) {
+                break;
+            }
+            __builtin_amdgcn_s_sleep(32);
+        }
+        if (o >= 0) {
+            for (;;) {
+                p = (int64_t)__hip_atomic_load((unsigned long long*)&a.ovf_idx[o], __ATOMIC_ACQUIRE,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                if (p >= 0) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
     }
     const int lo = __builtin_amdgcn_readfirstlane(__shfl((int)(p & 0xffffffff), 0, 64));
     const int hi = __builtin_amdgcn_readfirstlane(__shfl((int)(p >> 32), 0, 64));
@@ -282,10 +326,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
             p = a.park_idx[e];
             ent = (T*)a.park + (int64_t)e * a.park_stride;
         } else {
-            // the whole solve, in park entry blockIdx.x's workspace (the drain has finished)
+            // the whole solve, in park entry ent0 + blockIdx.x (this worker's own)
             p = take_overflow(a);
             if (p < 0) return;
-            ent = (T*)a.park + (int64_t)blockIdx.x * a.park_stride;
+            ent = (T*)a.park + (int64_t)(a.ent0 + blockIdx.x) * a.park_stride;
         }
         IpmProblem<T> pr;
 #pragma unroll
@@ -300,7 +344,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         else
             S.solve();
         S.finish_resto();
-        write_out(a, S, p, a.phase == 0 ? 1 : 2);
+        write_out(a, S, p, a.phase == 0 ? 1 : a.ovf_mark);
     }
 }
 
@@ -334,13 +378,12 @@ const void* resume_kernel_fn();
     X(8, 1, false, double, 1, false, 2)       \
     X(8, 1, false, double, 1, false, 1)       \
     X(9, 1, false, double, 2, false, 1)
+// (the fp32 solver's problems that need the restoration phase are solved again in fp64: its
+// resume kernel is the fp64 instance of the same horizon)
 #define MPCG_WIDE_RESUME_INSTANCES(X)         \
     X(1, 0, true, double, 1)                  \
     X(2, 0, false, double, 1)                 \
     X(3, 0, false, double, 2)                 \
-    X(4, 0, true, float, 1)                   \
-    X(5, 0, false, float, 1)                  \
-    X(6, 0, false, float, 2)                  \
     X(7, 1, true, double, 1)                  \
     X(8, 1, false, double, 1)                 \
     X(9, 1, false, double, 2)

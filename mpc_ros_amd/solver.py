@@ -22,8 +22,12 @@ IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor
 # Near the solution an fp32 iterate often cannot certify convergence (its dual residual
 # stalls): acceptable termination at 1e-3 and a 300-iteration cap end such stalls (measured
 # on the infinity set: the controls of those problems equal the fp64 solution to ~1e-5).
+# Where the fp32 solver's line search fails (a float iterate's noise floor) and Ipopt would enter
+# its feasibility-restoration phase, the problem is solved again from the start by the fp64
+# solver with the reference's options (no_restoration = 0; diag[:, 2] == 3 marks it); with
+# no_restoration = 1 it stops there with status 9.
 FP32_OPTIONS = dict(precision=1, tol=2e-4, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
-                    acceptable_tol=1e-3, max_iter=300, no_restoration=1)
+                    acceptable_tol=1e-3, max_iter=300, no_restoration=0)
 
 
 class BatchSolver:
@@ -169,6 +173,65 @@ class BatchSolver:
         _lib.check(_lib.lib().mpcg_track_device(
             self._h, B, M, ptr(pose), ptr(vel), ptr(plan), int(bool(delay_mode)), ptr(cmd), ptr(traj), ptr(status),
             C.c_void_p(stream.cuda_stream)), "mpcg_track_device")
+
+
+def _params_struct(params, dtype, ipopt):
+    if dtype == "fp32":
+        ipopt = dict(FP32_OPTIONS, **ipopt)
+    p = _lib.params_from_map(params if params is not None else PLUGIN_DEFAULTS)
+    opts = dict(IPOPT_DEFAULTS)
+    opts.update(ipopt)
+    for k, v in opts.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"mpcg_params has no field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+class MultiSolver:
+    """mpcg_multi: a persistent multi-GPU context (communicator, per-GPU handles, streams and
+    buffers for batches of up to B_max problems, created once); ``solve`` shards a host batch
+    over the GPUs and gathers the results to devices[0] by RCCL (include/mpcg.h)."""
+
+    def __init__(self, devices, B_max: int, params: dict | None = None, dtype: str = "fp64", **ipopt):
+        self.p = _params_struct(params, dtype, ipopt)
+        self.N = self.p.steps
+        self.B_max = int(B_max)
+        dev = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _lib.check(_lib.lib().mpcg_multi_create(len(devices), dev, C.byref(self.p), self.B_max, C.byref(h)),
+                   "mpcg_multi_create")
+        self._h = h
+
+    def solve(self, state, coeffs) -> dict:
+        state = np.ascontiguousarray(state, dtype=np.float64)
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+        B = state.shape[0]
+        assert state.shape == (B, 6) and coeffs.shape == (B, 4), "state [B,6], coeffs [B,4]"
+        N = self.N
+        u0 = np.zeros((B, 2))
+        traj = np.zeros((B, 3, N))
+        status = np.zeros(B, dtype=np.int32)
+        iters = np.zeros(B, dtype=np.int32)
+        obj = np.zeros(B)
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int32)
+        _lib.check(_lib.lib().mpcg_multi_solve(
+            self._h, B, state.ctypes.data_as(dp), coeffs.ctypes.data_as(dp), u0.ctypes.data_as(dp),
+            traj.ctypes.data_as(dp), status.ctypes.data_as(ip), obj.ctypes.data_as(dp), iters.ctypes.data_as(ip)),
+            "mpcg_multi_solve")
+        return dict(u0=u0, traj=traj, status=status, obj=obj, iters=iters)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().mpcg_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def solve_multi(devices, params: dict | None = None, state=None, coeffs=None, dtype: str = "fp64", **ipopt) -> dict:

@@ -246,6 +246,7 @@ struct ipm {
     double *wt, *yt, *zLt, *zUt;
     double *gf, *cv, *A, *W, *gphi, *rd, *ct, *csoc, *gft, *At, *rdt;
     double *KKT, *rhs;
+    double* KKT0;      /* refine_steps > 0: the matrix before its factorisation */
     int* ipiv;
     double mu, tau, dw_last;
     /* statistics of the current iterate */
@@ -311,6 +312,7 @@ static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
     TAKE(acc_w, nw); TAKE(acc_y, m); TAKE(acc_zL, nw); TAKE(acc_zU, nw);
 #undef TAKE
     S->ipiv = (int*)malloc(sizeof(int) * K);
+    if (o->refine_steps > 0) S->KKT0 = (double*)malloc(sizeof(double) * K * K + sizeof(double) * 2 * K);
     S->capf = 64;
     S->fth = (double*)malloc(sizeof(double) * S->capf);
     S->fph = (double*)malloc(sizeof(double) * S->capf);
@@ -322,6 +324,7 @@ static void ipm_alloc(ipm* S, iprob* P, const ora_ipm_opts* o) {
     S->last_mu = -1.0;
 }
 static void ipm_free(ipm* S) {
+    free(S->KKT0);
     free(S->kpos);
     free(S->klast);
     free(S->mem);
@@ -588,6 +591,7 @@ static int factor_kkt(ipm* S) {
             S->KKT[(nw + r) + (size_t)(nw + r) * K] = -delta_c;
         }
         int np, nn, nz;
+        if (S->KKT0) memcpy(S->KKT0, S->KKT, sizeof(double) * (size_t)K * K);
         ora_ldlt_factor(K, S->KKT, S->ipiv, 1e-300, &np, &nn, &nz);
         if (np == nw && nn == m && nz == 0) {
             if (delta_w > 0) S->dw_last = delta_w;
@@ -619,6 +623,33 @@ static void solve_step(ipm* S, const double* crhs, double* dw, double* dy, doubl
         for (int i = 0; i < S->K; ++i) b[S->kpos[i]] = S->rhs[i];
         ora_ldlt_solve_env(S->K, S->KKT, S->ipiv, S->klast, b);
         for (int i = 0; i < S->K; ++i) S->rhs[i] = b[S->kpos[i]];
+    } else if (S->KKT0) {
+        /* PDFullSpaceSolver::Solve's iterative refinement: residual r = b - K x of the
+         * unfactored matrix (lower triangle, symmetric), correction K c = r, x += c; at least
+         * refine_steps steps, more while |r| / (|x| + |b|) > 1e-10, at most 10 */
+        const int K = S->K;
+        double* b = S->KKT0 + (size_t)K * K;
+        double* r = b + K;
+        memcpy(b, S->rhs, sizeof(double) * K);
+        ora_ldlt_solve(K, S->KKT, S->ipiv, S->rhs);
+        for (int step = 0; step < 10; ++step) {
+            for (int i = 0; i < K; ++i) r[i] = b[i];
+            for (int j = 0; j < K; ++j) {
+                const double xj = S->rhs[j];
+                r[j] -= S->KKT0[j + (size_t)j * K] * xj;
+                for (int i = j + 1; i < K; ++i) {
+                    const double a = S->KKT0[i + (size_t)j * K];
+                    if (a != 0.0) {
+                        r[i] -= a * xj;
+                        r[j] -= a * S->rhs[i];
+                    }
+                }
+            }
+            const double ratio = amax(K, r) / (amax(K, S->rhs) + amax(K, b));
+            if (step >= S->o->refine_steps && !(ratio > 1e-10)) break;
+            ora_ldlt_solve(K, S->KKT, S->ipiv, r);
+            for (int i = 0; i < K; ++i) S->rhs[i] += r[i];
+        }
     } else {
         ora_ldlt_solve(S->K, S->KKT, S->ipiv, S->rhs);
     }

@@ -103,6 +103,11 @@ typedef struct ora_ipm_opts {
      * Ipopt + MUMPS on this band, for the CPU baseline; same algorithm, iterates equal
      * to rounding (a different pivot order) */
     int kkt_structured;
+    /* Ipopt's iterative refinement of each KKT solve (PDFullSpaceSolver: min_refinement_steps 1,
+     * max_refinement_steps 10, residual_ratio_max 1e-10) on the dense path: 0 (default, the
+     * pinned fixtures) = none; k > 0 = at least k steps, more while the residual ratio exceeds
+     * 1e-10, at most 10 -- restated in round 4 to measure what omitting it changes */
+    int refine_steps;
 } ora_ipm_opts;
 
 /* Result; status uses CppAD::ipopt::solve_result::status_type numbering

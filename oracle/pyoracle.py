@@ -38,7 +38,7 @@ class IpmOpts(C.Structure):
         ("restoration", C.c_int), ("obj_max_inc", C.c_double), ("max_filter_resets", C.c_int),
         ("filter_reset_trigger", C.c_int), ("tiny_step_tol", C.c_double), ("tiny_step_y_tol", C.c_double),
         ("cpu_iter_budget", C.c_int), ("dual_inf_tol", C.c_double), ("constr_viol_tol", C.c_double),
-        ("compl_inf_tol", C.c_double), ("kkt_structured", C.c_int),
+        ("compl_inf_tol", C.c_double), ("kkt_structured", C.c_int), ("refine_steps", C.c_int),
     ]
 
 

@@ -175,3 +175,32 @@ def test_multi_gpu_shard_and_gather_plan(libmpcg):
         assert (cover == 1).all()
     assert libmpcg.mpcg_shard_range(10, 2, 2, C.byref(start), C.byref(count)) < 0
     assert libmpcg.mpcg_last_error()
+
+
+def test_multi_context_buffers_and_no_gpu(libmpcg):
+    """The persistent multi-GPU context's per-GPU device buffers (mpcg_multi_buffer_bytes): every
+    GPU holds the inputs of the largest shard (80 B per problem); the root the gathered outputs
+    of B_max problems, the others their shard's outputs (32 + 24 N B per problem) -- summed
+    over the GPUs, the outputs are B_max + (G - 1) largest shards.  Creating a context without a
+    GPU fails with an error, never a CPU fallback."""
+    import torch
+
+    for B, G, N in ((524288, 8, 20), (65537, 8, 40), (7, 3, 20), (2, 4, 20), (1, 1, 3)):
+        cmax = -(-B // G)
+        per_out = 32 + 24 * N
+        for r in range(G):
+            got = libmpcg.mpcg_multi_buffer_bytes(B, N, G, r)
+            out = (B if r == 0 else cmax) * per_out
+            assert got == 80 * max(cmax, 1) + max(out, 1)
+    assert libmpcg.mpcg_multi_buffer_bytes(10, 20, 2, 2) == 0 and libmpcg.mpcg_multi_buffer_bytes(10, 0, 2, 0) == 0
+    if torch.cuda.is_available():
+        return
+    from mpc_ros_amd import _lib
+
+    p = _lib.MpcgParams()
+    libmpcg.mpcg_params_plugin_default(C.byref(p))
+    dev = (C.c_int * 2)(0, 1)
+    h = C.c_void_p()
+    assert libmpcg.mpcg_multi_create(2, dev, C.byref(p), 1024, C.byref(h)) < 0 and not h.value
+    assert libmpcg.mpcg_last_error()
+    libmpcg.mpcg_multi_destroy(None)

@@ -360,6 +360,30 @@ def test_solve_multi_one_gpu_matches_single(torch_cuda, infinity_golden):
         np.testing.assert_array_equal(r[k], s[k])
 
 
+def test_multi_context_matches_single(torch_cuda, infinity_golden):
+    """The persistent multi-GPU context (mpcg_multi: communicator, handles and buffers created
+    once) on the GPUs of this box: several batches of different sizes through one context
+    equal the single-handle solve bitwise; a batch above its B_max is refused."""
+    import torch
+
+    from mpc_ros_amd._lib import MpcgError
+    from mpc_ros_amd.solver import MultiSolver
+
+    g = infinity_golden
+    P = params_from_array(g["params"])
+    devs = list(range(torch.cuda.device_count()))
+    m = MultiSolver(devs, 288, P)
+    s = solver_for(P)
+    for B in (288, 5, 131):
+        r = m.solve(g["state"][:B], g["coeffs"][:B])
+        ref = s.solve(g["state"][:B], g["coeffs"][:B])
+        for k in ("u0", "traj", "status", "iters", "obj"):
+            np.testing.assert_array_equal(r[k], ref[k])
+    with pytest.raises(MpcgError):
+        m.solve(np.zeros((289, 6)), np.zeros((289, 4)))
+    m.close()
+
+
 def test_default_option_instance_equals_general(torch_cuda, features_golden, oracle):
     """The kernel instance that compiles the reference's (default) Ipopt options as
     constants and the general instance (taken for any other option values) run the same

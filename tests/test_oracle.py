@@ -235,3 +235,27 @@ def test_structured_kkt_same_iterates(oracle, infinity_golden):
     np.testing.assert_array_equal(r["iters"], g["iters"][sel])
     ok = g["status"][sel] == 1
     np.testing.assert_allclose(r["u0"][ok], g["u0"][sel][ok], rtol=0, atol=1e-12)
+
+
+def test_iterative_refinement_changes_no_fixture_row(oracle, infinity_golden, features_golden):
+    """Ipopt refines every KKT solve at least once (PDFullSpaceSolver, min_refinement_steps 1,
+    residual_ratio_max 1e-10); the oracle's fixtures and the device solve without it.  With the
+    refinement restated (ora_ipm_opts.refine_steps = 1) the infinity set and every Ipopt-feature
+    set (SOC, watchdog, soft restoration, the restoration phase at N = 20 and 40, the bicycle)
+    keep every status, iteration count and restoration count, and u0 moves by rounding only
+    (measured: <= 3.2e-15): omitting it changes no parity claim on these problems.  (The
+    locally infeasible small_bound variant, 5-13 restoration phases at condition numbers
+    ~1e13, is the exception: one row of 16 takes 68 iterations instead of 67, u0 within 1e-11
+    -- tests/test_core_host.py compare_infeasible.)"""
+    sets = [("infinity", infinity_golden, 20, slice(0, 96))]
+    for name in ("N20", "N40", "bicycle", "resto_N20", "resto_N40"):
+        g = features_golden[name]
+        sets.append((name, g, int(g["P"]["STEPS"]), slice(None)))
+    for name, g, N, sl in sets:
+        P = g["P"] if "P" in g else params_from_array(g["params"])
+        r = oracle.mpc_solve_batch(P, g["state"][sl], g["coeffs"][sl], opts=oracle.ref_opts(N, refine_steps=1),
+                                   nthreads=8, diag=True)
+        np.testing.assert_array_equal(r["status"], g["status"][sl], err_msg=name)
+        np.testing.assert_array_equal(r["iters"], g["iters"][sl], err_msg=name)
+        np.testing.assert_array_equal(r["diag"][:, 3], g["diag"][sl, 3], err_msg=name)
+        np.testing.assert_allclose(r["u0"], g["u0"][sl], rtol=0, atol=1e-13, err_msg=name)
