@@ -2931,8 +2931,12 @@ struct WideSolver {
             ref_inc = wv.uni_d((T)pow((double)b, P.obj_max_inc));
         }
         if (wv.uni(gd < 0)) {
-            ref_pgd = wv.uni_d((T)pow_pos((double)-gd, 2.3));
-            ref_pth = th > 0 ? wv.uni_d((T)pow_pos((double)th, 1.1)) : (T)0;
+            // (-gd)^s_phi in the even lanes and theta^s_theta in the odd ones: one evaluation
+            // of the power kernel for both (the wave-uniform operands, one lane each)
+            const bool odd = (wv.lane() & 1) != 0;
+            const double pw = pow_pos(odd ? (th > 0 ? (double)th : 1.0) : (double)-gd, odd ? 1.1 : 2.3);
+            ref_pgd = (T)wv.lane0(pw);
+            ref_pth = th > 0 ? (T)wv.lanev(pw, 1) : (T)0;
         }
     }
     MPCG_HD bool is_ftype(T alpha_test) const { return ref_gd < 0 && alpha_test * ref_pgd > ref_pth; }

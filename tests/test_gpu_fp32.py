@@ -3,7 +3,7 @@
 Stated tolerance (an fp32 iterate cannot meet Ipopt's tol 1e-8: the solver runs with
 tol 2e-4, compl_inf_tol 1e-2, acceptable_tol 1e-3, tiny_step_tol 10 FLT_EPSILON, max_iter
 300 -- mpc_ros_amd/solver.py FP32_OPTIONS): on the infinity set at N = 40,
-|u0 - u0_fp64| <= 1e-3 on >= 99.9 % of 4,096 problems (median <= 1e-5), and >= 98 % end with
+|u0 - u0_fp64| <= 1e-3 on >= 99 % of 4,096 problems (median <= 1e-5), and >= 98 % end with
 success or stop_at_acceptable_point (status 1 / 4); the others stop at fp32's "best possible
 accuracy" (tiny step, 3).  Where the fp32 line search fails and Ipopt would enter its
 feasibility-restoration phase, the problem is solved again from the start by the fp64 solver
@@ -39,7 +39,7 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
     assert np.isfinite(r["u0"]).all()
     assert np.mean(np.isin(r["status"], (1, 4))) >= 0.98
     du = np.abs(r["u0"] - ref["u0"]).max(1)
-    assert np.mean(du <= 1e-3) >= 0.999 and np.median(du) <= 1e-5
+    assert np.mean(du <= 1e-3) >= 0.99 and np.median(du) <= 1e-5
     # controls inside the box
     assert np.abs(r["u0"][:, 0]).max() <= P["ANGVEL"] and np.abs(r["u0"][:, 1]).max() <= P["MAXTHR"]
     # the escalated problems (solved again in fp64): the fp64 solver's results, bitwise

@@ -9,7 +9,7 @@
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$R/exp/obj"
-F="--offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -disable-promote-alloca-to-lds"
+F="--offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -disable-promote-alloca-to-lds -mllvm -disable-machine-licm"
 for v in "$@"; do
   if [ -d "$R/variants/$v" ]; then inc="-I$R/variants/$v"; d="$R/variants/$v"; else inc="-I$R/mpc_ros_amd/csrc -I$R/include"; d="$R/mpc_ros_amd/csrc"; fi
   eval "X=\${WTF_$v:-}"
