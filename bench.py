@@ -12,8 +12,10 @@ A step = one pass of the hot path over one batch: every rank solves its shard of
 B problems (BASELINE.json configs[3]: 524288 problems over 8 GPUs = 65536 per GPU,
 N = 20, fp64, differential drive) with the HIP kernel, then the controls and
 statuses are gathered to rank 0 (torch.distributed.gather: RCCL point-to-point over
-xGMI, each rank sends its slice only) -- the only exchange.  Inputs are resident in HBM before the timed region (weak scaling: the
-per-GPU batch is fixed).  Rank 0 prints one JSON line.
+xGMI, each rank sends its slice only) -- the only exchange.  Each rank generates its shard of
+the synthetic robots on its own GPU from (seed, global index) (mpcg_synth_infinity_device) and
+preprocesses them there (findBestPath, mpcg_preprocess_device); the inputs are resident in HBM
+before the timed region (weak scaling: the per-GPU batch is fixed).  Rank 0 prints one JSON line.
 
 roofline: the dominant kernel, mpcg::k_solve_wide (one problem per wavefront, whole
 problem state in LDS; the restoration phase's k_resume_wide runs beside it on a second
@@ -84,6 +86,10 @@ def parse():
     ap.add_argument("--restoration", default="auto", choices=["auto", "on", "off"],
                     help="Ipopt's feasibility-restoration phase: auto = the dtype's default (fp64 on; the fp32 "
                          "solver's FP32_OPTIONS off), on / off = mpcg_params.no_restoration 0 / 1")
+    ap.add_argument("--inputs", default="device", choices=["device", "host"],
+                    help="where each rank generates its shard of the synthetic robots from (seed, global index): "
+                         "device = mpcg_synth_infinity_device + the device preprocessing (findBestPath); host = "
+                         "infinity.py (numpy) and a copy in")
     ap.add_argument("--mode", default="solve", choices=["solve", "track"],
                     help="solve: MPC::Solve on preprocessed inputs (the metric); track: the whole control "
                          "tick from raw poses and waypoint plans (findBestPath + solve + post-processing)")
@@ -290,18 +296,28 @@ def main():
     if a.model == "bicycle":  # steering bound 0.5 rad, wheelbase 0.5 m (tests/golden/bicycle_N25.npz)
         P.update(MODEL=1, LF=0.5, ANGVEL=0.5)
     start, count = D.shard(total, rank, world)
-    st, cf = infinity.make_problems(np.arange(start, start + count))
-    tst = torch.from_numpy(st).to(dev)
-    tcf = torch.from_numpy(cf).to(dev)
-    if a.mode == "track":
-        sc = infinity.draw_scenarios(np.arange(start, start + count))
-        px, py, yaw, plan = infinity.scenario_poses(sc)
-        tpose = torch.from_numpy(np.ascontiguousarray(np.stack([px, py, yaw], 1))).to(dev)
-        tvel = torch.from_numpy(np.ascontiguousarray(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))).to(dev)
-        tplan = torch.from_numpy(np.ascontiguousarray(plan)).to(dev)
-        cmd = torch.empty((count, 3), dtype=torch.float64, device=dev)
     extra = {} if a.restoration == "auto" else {"no_restoration": int(a.restoration == "off")}
     solver = BatchSolver(dev.index, P, strategy=a.strategy, dtype=a.dtype, **extra)
+    if a.inputs == "device":
+        # this rank's robots from (seed, global index) on its GPU, preprocessed there
+        tpose, tvel, tplan = solver.synth_infinity_device(start, count)
+        tst = torch.empty((count, 6), dtype=torch.float64, device=dev)
+        tcf = torch.empty((count, 4), dtype=torch.float64, device=dev)
+        solver.preprocess_device(tpose, tvel, tplan, tst, tcf)
+        torch.cuda.synchronize()
+        st, cf = (tst.cpu().numpy(), tcf.cpu().numpy()) if rank == 0 else (None, None)
+    else:
+        st, cf = infinity.make_problems(np.arange(start, start + count))
+        tst = torch.from_numpy(st).to(dev)
+        tcf = torch.from_numpy(cf).to(dev)
+        if a.mode == "track":
+            sc = infinity.draw_scenarios(np.arange(start, start + count))
+            px, py, yaw, plan = infinity.scenario_poses(sc)
+            tpose = torch.from_numpy(np.ascontiguousarray(np.stack([px, py, yaw], 1))).to(dev)
+            tvel = torch.from_numpy(np.ascontiguousarray(np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))).to(dev)
+            tplan = torch.from_numpy(np.ascontiguousarray(plan)).to(dev)
+    if a.mode == "track":
+        cmd = torch.empty((count, 3), dtype=torch.float64, device=dev)
     solver.reserve(count)
     u0 = torch.empty((count, 2), dtype=torch.float64, device=dev)
     traj = torch.empty((count, 3, N), dtype=torch.float64, device=dev)
@@ -410,7 +426,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64" if a.dtype == "fp64" else "f32",
-            "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem)",
+            "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem, "
+                    + ("generated per rank on its GPU)" if a.inputs == "device" else "generated on the host)"),
             "config": {"workload": f"{'diff-drive' if a.model == 'diffdrive' else 'kinematic-bicycle'} NMPC "
                                    f"(MPC::Solve NLP, Ipopt algorithm), N={N}, {a.dtype}, "
                                    f"{B} problems per GPU (BASELINE configs[3] shard), gather to rank 0",

@@ -255,6 +255,16 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
                       const double* d_plan, int32_t delay_mode, double* d_cmd, double* d_traj, int32_t* d_status,
                       void* stream);
 
+/* The benchmark's synthetic robots (the "infinity set", mpc_ros_amd/infinity.py) generated on
+ * the device: robot start + i of the set (i < B) is a pure function of (seed, start + i) --
+ * a pose near a lemniscate course, its speed and previous controls, and a plan of M waypoints
+ * along the course -- so a rank of a multi-GPU run generates exactly its own slice on its GPU.
+ * Outputs as mpcg_preprocess_device takes them: pose [B][3], vel [B][3], plan [B][M][2].  Not
+ * part of the reference's interface (a data generator for benchmarks and tests); queued on
+ * `stream` (the first call uploads a 3.2 MB table synchronously). */
+int mpcg_synth_infinity_device(mpcg_handle* h, uint64_t seed, int64_t start, int64_t B, int32_t M, double* d_pose,
+                               double* d_vel, double* d_plan, void* stream);
+
 /* Kernel strategy of the handle's solves.  Since ABI 2 there is one: one problem per
  * wavefront, the whole problem state in LDS (AUTO and WAVE select it).  LANE (the round-1
  * one-problem-per-lane kernels) was removed; selecting it is an error. */

@@ -91,6 +91,8 @@ SIGNATURES = {
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
     "mpcg_set_park_capacity": ([C.c_void_p, C.c_int64], C.c_int),
     "mpcg_last_kernel": ([C.c_void_p], C.c_char_p),
+    "mpcg_synth_infinity_device": ([C.c_void_p, C.c_uint64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p], C.c_int),
 }
 
 STRATEGY = {"auto": 0, "lane": 1, "wave": 2}  # (LANE was removed in ABI 2: selecting it raises)

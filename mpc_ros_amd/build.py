@@ -12,8 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmpcg.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_wide_inst.hip", "mpcg_track.hip", "mpcg_api.cpp",
-                                           "mpcg_multi.cpp", "mpc_planner.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_wide_inst.hip", "mpcg_track.hip", "mpcg_synth.hip",
+                                           "mpcg_api.cpp", "mpcg_multi.cpp", "mpc_planner.cpp")]
 INST = os.path.join(CSRC, "mpcg_wide_inst.hip")
 N_INST = 10  # MPCG_INST groups of mpcg_wide_inst.hip (mpcg_wide_kern.h)
 HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h",

@@ -64,6 +64,8 @@ struct mpcg_handle {
     const char* last_kernel = "";
     // park-area entries (0: the default, max(256, B / 128))
     int64_t park_cap = 0;
+    // the synthetic robots' arc-length table (mpcg_synth_infinity_device), uploaded once
+    double* d_arc = nullptr;
 };
 
 #ifndef MPCG_BUILD_ID
@@ -323,6 +325,7 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->d_pp) hipFree(h->d_pp);
     if (h->d_sched) hipFree(h->d_sched);
     if (h->d_spill) hipFree(h->d_spill);
+    if (h->d_arc) hipFree(h->d_arc);
     if (h->aux) hipStreamSynchronize(h->aux);
     if (h->last_ev) hipEventDestroy(h->last_ev);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -603,6 +606,35 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
 }
 
 const char* mpcg_last_kernel(const mpcg_handle* h) { return h ? h->last_kernel : ""; }
+
+int mpcg_synth_infinity_device(mpcg_handle* h, uint64_t seed, int64_t start, int64_t B, int32_t M, double* d_pose,
+                               double* d_vel, double* d_plan, void* stream) {
+    if (!h) return fail(-1, "null handle");
+    if (B < 0 || start < 0) return fail(-1, "negative batch or start");
+    if (B == 0) return 0;
+    if (M < 4) return fail(-1, "M (waypoints per robot) must be >= 4");
+    if (!d_pose || !d_vel || !d_plan) return fail(-1, "null buffer");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    const int n = mpcg::synth_arc_len();
+    if (!h->d_arc) {
+        std::vector<double> t, s;
+        mpcg::synth_arc_table(t, s);
+        e = hipMalloc((void**)&h->d_arc, sizeof(double) * 2 * n);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(arc table)");
+        e = hipMemcpy(h->d_arc, t.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->d_arc + n, s.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            hipFree(h->d_arc);
+            h->d_arc = nullptr;
+            return hip_fail(e, "hipMemcpy(arc table)");
+        }
+    }
+    e = mpcg::launch_synth_infinity(seed, start, B, M, h->d_arc, h->d_arc + n, d_pose, d_vel, d_plan,
+                                    (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "synthetic robots launch");
+    return 0;
+}
 
 int mpcg_set_park_capacity(mpcg_handle* h, int64_t cap) {
     if (!h) return fail(-1, "null handle");

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "ipm_core.h"
 
@@ -42,6 +43,13 @@ hipError_t launch_find_best_path(int64_t B, int M, double dt, int delay_mode, co
                                  const double* plan, double* state, double* coeffs, double* ws, hipStream_t stream);
 hipError_t launch_post(int64_t B, double dt, double ref_v, const double* vel, const double* u0, double* cmd,
                        hipStream_t stream);
+
+// The benchmark's synthetic robots (mpcg_synth.hip): the lemniscate's arc-length table (host,
+// once) and the per-robot pose / velocities / plan from (seed, global index)
+void synth_arc_table(std::vector<double>& t, std::vector<double>& s);
+int synth_arc_len();
+hipError_t launch_synth_infinity(uint64_t seed, int64_t start, int64_t B, int M, const double* arc_t,
+                                 const double* arc_s, double* pose, double* vel, double* plan, hipStream_t stream);
 
 }  // namespace mpcg
 #endif

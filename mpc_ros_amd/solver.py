@@ -138,6 +138,26 @@ class BatchSolver:
             self._h, B, ptr(state), ptr(coeffs), ptr(u0), ptr(traj), ptr(status), ptr(obj), ptr(iters), ptr(diag),
             C.c_void_p(stream.cuda_stream)), "mpcg_solve_device_ex")
 
+    # ------------------------------------------------ the benchmark's synthetic robots
+    def synth_infinity_device(self, start: int, B: int, M: int = 11, seed: int | None = None, stream=None):
+        """Robots start .. start + B - 1 of the infinity set generated on this GPU from (seed,
+        global index) (mpcg_synth_infinity_device): torch tensors pose [B,3], vel [B,3], plan [B,M,2]."""
+        import torch
+
+        from . import infinity
+
+        dev = torch.device("cuda", self.device)
+        pose = torch.empty((B, 3), dtype=torch.float64, device=dev)
+        vel = torch.empty((B, 3), dtype=torch.float64, device=dev)
+        plan = torch.empty((B, M, 2), dtype=torch.float64, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        _lib.check(_lib.lib().mpcg_synth_infinity_device(
+            self._h, int(infinity.SEED if seed is None else seed), int(start), int(B), int(M), C.c_void_p(pose.data_ptr()),
+            C.c_void_p(vel.data_ptr()), C.c_void_p(plan.data_ptr()), C.c_void_p(stream.cuda_stream)),
+            "mpcg_synth_infinity_device")
+        return pose, vel, plan
+
     # ------------------------------------------------ the caller side on the device
     def preprocess_device(self, pose, vel, plan, state, coeffs, delay_mode: bool = True, stream=None):
         """Tracking::findBestPath's preprocessing (driving_state.cpp:175-256) for B robots.

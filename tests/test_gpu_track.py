@@ -225,3 +225,31 @@ def test_two_streams_share_one_handle(torch_cuda):
     torch.cuda.synchronize()
     for o, r in zip(outs, solo):
         np.testing.assert_array_equal(o.cpu().numpy(), r)
+
+
+def test_synthetic_robots_on_device_match_host_generator(torch_cuda):
+    """mpcg_synth_infinity_device: the benchmark's robots generated on the GPU from (seed, global
+    index) equal infinity.py's host generator (the integer hash bitwise, the trigonometry within
+    rounding), for a slice that does not start at 0 (a rank's shard); through the device
+    preprocessing they give MPC::Solve's inputs of infinity.make_problems."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity, params
+
+    P = params.PLUGIN_DEFAULTS
+    s = _solver(P)
+    start, B = 3 * 65536 + 17, 4096
+    pose, vel, plan = s.synth_infinity_device(start, B)
+    torch.cuda.synchronize()
+    idx = np.arange(start, start + B)
+    sc = infinity.draw_scenarios(idx)
+    px, py, yaw, hplan = infinity.scenario_poses(sc)
+    np.testing.assert_allclose(pose.cpu().numpy(), np.stack([px, py, yaw], 1), rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(vel.cpu().numpy(), np.stack([sc["v"], sc["w_prev"], sc["a_prev"]], 1))
+    np.testing.assert_allclose(plan.cpu().numpy(), hplan, rtol=0, atol=1e-12)
+    st = torch.empty((B, 6), dtype=torch.float64, device=pose.device)
+    cf = torch.empty((B, 4), dtype=torch.float64, device=pose.device)
+    s.preprocess_device(pose, vel, plan, st, cf)
+    torch.cuda.synchronize()
+    hst, hcf = infinity.make_problems(idx)
+    np.testing.assert_allclose(st.cpu().numpy(), hst, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(cf.cpu().numpy(), hcf, rtol=1e-9, atol=1e-9)
