@@ -145,7 +145,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     S.solve();
-    if (S.status == Solver::NEED_RESTO) {
+    // the fp32 solver's problems it cannot finish -- the line search fails where Ipopt would
+    // enter its restoration phase, or it stops at a tiny step or the iteration limit (a float
+    // iterate's noise floor) -- are solved again by the fp64 solver (escalation, unless
+    // no_restoration: the park area is empty for it, so they go to the overflow list)
+    const bool escalate = sizeof(T) == 4 && !Pk.no_resto && (S.status == IPM_TINY_STEP || S.status == IPM_MAXITER);
+    if (S.status == Solver::NEED_RESTO || escalate) {
         // the restoration phase runs in k_resume_wide: park the problem
         int e = 0;
         if (t == 0) e = atomicAdd(a.park_count, 1);
