@@ -209,6 +209,9 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
 #define MPCG_RESUME_WORKERS 2
 #endif
 static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 65536; }
+// the fp32 solver's escalations are ~100x more frequent (~2e-3 of the infinity set at N = 40,
+// 7e-3 at N = 20): 8 workers and one more per 8,192 problems take them while the batch runs
+static int64_t escalation_workers(int64_t B) { return 8 + B / 8192; }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
@@ -280,7 +283,8 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     // branches need not run concurrently: the workers then exit at once (take_parked) and
     // the drain takes every parked problem.
     const bool fork = aux && aux != stream && ev_fork && ev_join;
-    const unsigned workers = fork ? (unsigned)(pc < resume_workers(B) ? pc : resume_workers(B)) : 0u;
+    const int64_t nw = esc ? escalation_workers(B) : resume_workers(B);
+    const unsigned workers = fork ? (unsigned)(pc < nw ? pc : nw) : 0u;
     if (fork) {
         e = hipEventRecord(ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);
