@@ -25,7 +25,7 @@ cfg)
     case $c in n20) a="";; b4096) a="--batch 4096";; n40) a="--horizon 40";; n40f32) a="--horizon 40 --dtype fp32";;
       n40f32r) a="--horizon 40 --dtype fp32 --restoration on";; n20f32) a="--dtype fp32";; bic25) a="--model bicycle --horizon 25";;
       track) a="--mode track";; n100) a="--batch 4096 --horizon 100";; n64) a="--horizon 64";; bic40) a="--model bicycle --horizon 40";;
-      b1024) a="--batch 1024";; lat) a="--batch 4096 --cpu-seconds 1";; esac
+      b1024) a="--batch 1024";; lat) a="--batch 4096 --cpu-seconds 1";; n40f32off) a="--horizon 40 --dtype fp32 --restoration off";; esac
     timeout -k 10 300 python bench.py --steps ${CSTEPS:-10} --warmup 2 --cpu-seconds 0 $a > $O/cfg_$c.log 2>&1; rc=$?
     [ "$c" = lat ] && { timeout -k 10 300 python bench.py --steps 5 --warmup 1 $a > $O/cfg_$c.log 2>&1; rc=$?; }
     echo "$c rc=$rc"; [ $rc -eq 0 ] || exit 1
