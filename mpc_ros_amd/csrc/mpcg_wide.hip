@@ -2,6 +2,8 @@
 // launch side (solve order, instance choice, workspace, batch kernel + resume workers).
 // The kernels are in mpcg_wide_kern.h, their instances in mpcg_wide_inst.hip.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <hipcub/device/device_radix_sort.hpp>
 
 #include "mpcg_wide_kern.h"
@@ -209,9 +211,19 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
 #define MPCG_RESUME_WORKERS 2
 #endif
 static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 65536; }
-// the fp32 solver's escalations are ~100x more frequent (~2e-3 of the infinity set at N = 40,
-// 7e-3 at N = 20): 8 workers and one more per 8,192 problems take them while the batch runs
-static int64_t escalation_workers(int64_t B) { return 8 + B / 8192; }
+// the fp32 solver's escalations are ~30x more frequent (1.7e-2 of the infinity set at N = 40:
+// 1,127 of 65,536): they are taken while the batch runs by 8 workers and one more per 512
+// problems (136 at 65,536), so few are left for the drain -- each worker holds a SIMD for the
+// batch (13 % of the device at 65,536), but measured at N = 40 the launch takes 35.1 ms with
+// 136 workers, 41.4 ms with 16, 40.0 with 72, 35.4-37.2 with 176-512 (N = 20: 14.95 / 16.15 ms
+// with 136 / 16).  MPCG_ESCALATION_WORKERS overrides the count (a tuning knob, read once).
+static int64_t escalation_workers(int64_t B) {
+    static const int64_t env = [] {
+        const char* s = getenv("MPCG_ESCALATION_WORKERS");
+        return s ? (int64_t)atoll(s) : (int64_t)-1;
+    }();
+    return env > 0 ? env : 8 + B / 512;
+}
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,

@@ -145,11 +145,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     S.solve();
-    // the fp32 solver's problems whose line search fails at a float iterate's noise floor --
-    // where Ipopt would enter its restoration phase (NEED_RESTO), or almost feasible without an
-    // acceptable point (RESTORATION_FAILURE) -- are solved again by the fp64 solver (escalation,
-    // unless no_restoration: the park area is empty for it, so they go to the overflow list)
-    const bool escalate = sizeof(T) == 4 && !Pk.no_resto && S.status == IPM_RESTORATION_FAILURE;
+    // the fp32 solver's problems it cannot finish at a float iterate's noise floor -- the line
+    // search fails where Ipopt would enter its restoration phase (NEED_RESTO) or almost feasible
+    // without an acceptable point (RESTORATION_FAILURE), or it stops at a tiny step or the
+    // iteration limit -- are solved again by the fp64 solver (escalation, unless no_restoration:
+    // the park area is empty for it, so they go to the overflow list)
+    const bool escalate = sizeof(T) == 4 && !Pk.no_resto &&
+                          (S.status == IPM_RESTORATION_FAILURE || S.status == IPM_TINY_STEP || S.status == IPM_MAXITER);
     if (S.status == Solver::NEED_RESTO || escalate) {
         // the restoration phase runs in k_resume_wide: park the problem
         int e = 0;

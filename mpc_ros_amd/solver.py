@@ -22,10 +22,12 @@ IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor
 # Near the solution an fp32 iterate often cannot certify convergence (its dual residual
 # stalls): acceptable termination at 1e-3 and a 300-iteration cap end such stalls (measured
 # on the infinity set: the controls of those problems equal the fp64 solution to ~1e-5).
-# Where the fp32 solver's line search fails (a float iterate's noise floor) -- Ipopt would enter
-# its feasibility-restoration phase, or it is almost feasible without an acceptable point --
-# the problem is solved again from the start by the fp64 solver with the reference's options
-# (no_restoration = 0; diag[:, 2] == 3 marks it); with no_restoration = 1 it stops with status 9.
+# Where the fp32 solver cannot finish -- its line search fails (a float iterate's noise floor)
+# where Ipopt would enter its feasibility-restoration phase, or it is almost feasible without an
+# acceptable point, or it stops at a tiny step or the iteration limit -- the problem is solved
+# again from the start by the fp64 solver with the reference's options (no_restoration = 0;
+# diag[:, 2] == 3 marks it; 1.7 % of the infinity set at N = 40); with no_restoration = 1 it
+# keeps the fp32 ending (status 9, 3 or 2).
 FP32_OPTIONS = dict(precision=1, tol=2e-4, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
                     acceptable_tol=1e-3, max_iter=300, no_restoration=0)
 

@@ -3,14 +3,15 @@
 Stated tolerance (an fp32 iterate cannot meet Ipopt's tol 1e-8: the solver runs with
 tol 2e-4, compl_inf_tol 1e-2, acceptable_tol 1e-3, tiny_step_tol 10 FLT_EPSILON, max_iter
 300 -- mpc_ros_amd/solver.py FP32_OPTIONS): on the infinity set at N = 40,
-|u0 - u0_fp64| <= 1e-3 on >= 99 % of 4,096 problems (median <= 1e-5), and >= 98 % end with
-success or stop_at_acceptable_point (status 1 / 4); the rest stop at a tiny step (3), the float
-iterate's "best possible accuracy".  The rows beyond 1e-3 (0.56 % measured) are converged fp32
-solves (status 1) that met tol 2e-4 a few iterations before the fp64 solve met 1e-8: the
-tolerance, not a failure (tools/fp32_diag.py).  Where the fp32 line search fails -- Ipopt
-would enter its feasibility-restoration phase, or it is almost feasible without an acceptable
-point -- the problem is solved again from the start by the fp64 solver (diag[:, 2] == 3):
-those rows equal the fp64 solver's bitwise.
+|u0 - u0_fp64| <= 1e-3 on >= 99 % of 4,096 problems (median <= 1e-5), and >= 99.5 % end with
+success or stop_at_acceptable_point (status 1 / 4; measured: all).  The rows beyond 1e-3
+(0.56 % measured) are converged fp32 solves (status 1) that met tol 2e-4 with compl_inf_tol
+1e-2 a few iterations before the fp64 solve met 1e-8: the tolerance, not a failure
+(tools/fp32_diag.py; compl_inf_tol 1e-3 brings them to 0.2 % at 3x the escalations).  Where
+the fp32 solver cannot finish -- its line search fails where Ipopt would enter its
+feasibility-restoration phase, or almost feasible without an acceptable point, or it stops at
+a tiny step or the iteration limit -- the problem is solved again from the start by the fp64
+solver (diag[:, 2] == 3): those rows equal the fp64 solver's bitwise.
 """
 from __future__ import annotations
 
@@ -40,7 +41,7 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
     ref = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ref_opts(40), nthreads=16)
     r = BatchSolver(0, P, dtype="fp32").solve(st, cf)
     assert np.isfinite(r["u0"]).all()
-    assert np.mean(np.isin(r["status"], (1, 4))) >= 0.98 and not np.isin(r["status"], (9, 10)).any()
+    assert np.mean(np.isin(r["status"], (1, 4))) >= 0.995 and not np.isin(r["status"], (2, 3, 9, 10)).any()
     du = np.abs(r["u0"] - ref["u0"]).max(1)
     assert np.mean(du <= 1e-3) >= 0.99 and np.median(du) <= 1e-5
     # controls inside the box
@@ -55,8 +56,9 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
 
 
 def test_fp32_no_restoration_option(torch_cuda):
-    """no_restoration = 1: the fp32 solver stops with status 9 where it would escalate; every
-    other row is the same."""
+    """no_restoration = 1: the fp32 solver keeps its own ending where it would escalate --
+    status 9 where Ipopt would restore, 3 at a tiny step, 2 at the iteration limit; every other
+    row is the same."""
     from mpc_ros_amd import infinity, params
     from mpc_ros_amd.solver import BatchSolver
 
@@ -65,8 +67,8 @@ def test_fp32_no_restoration_option(torch_cuda):
     a = BatchSolver(0, P, dtype="fp32").solve(st, cf)
     b = BatchSolver(0, P, dtype="fp32", no_restoration=1).solve(st, cf)
     esc = a["diag"][:, 2] == 3
-    assert (b["diag"][:, 2] == 0).all() and (b["status"][esc] == 9).all()
-    assert not (b["status"][~esc] == 9).any()
+    assert (b["diag"][:, 2] == 0).all() and np.isin(b["status"][esc], (2, 3, 9)).all()
+    assert not np.isin(b["status"][~esc], (2, 3, 9)).any()
     np.testing.assert_array_equal(a["status"][~esc], b["status"][~esc])
     np.testing.assert_array_equal(a["u0"][~esc], b["u0"][~esc])
 
