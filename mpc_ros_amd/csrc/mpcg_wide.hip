@@ -210,7 +210,14 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
 #ifndef MPCG_RESUME_WORKERS
 #define MPCG_RESUME_WORKERS 2
 #endif
-static int64_t resume_workers(int64_t B) { return MPCG_RESUME_WORKERS + B / 65536; }
+// (MPCG_RESUME_WORKERS in the environment overrides the count: a tuning knob, read once)
+static int64_t resume_workers(int64_t B) {
+    static const int64_t env = [] {
+        const char* s = getenv("MPCG_RESUME_WORKERS");
+        return s ? (int64_t)atoll(s) : (int64_t)-1;
+    }();
+    return env > 0 ? env : MPCG_RESUME_WORKERS + B / 65536;
+}
 // the fp32 solver's escalations are ~30x more frequent (1.7e-2 of the infinity set at N = 40:
 // 1,127 of 65,536): they are taken while the batch runs by 8 workers and one more per 512
 // problems (136 at 65,536), so few are left for the drain -- each worker holds a SIMD for the
