@@ -1,10 +1,14 @@
 // tests/native/wide_host_check.cpp -- TEST HARNESS ONLY.
 //
 // Runs the one-problem-per-wavefront solver (mpc_ros_amd/csrc/wide_core.h) on the
-// host: the 64 lanes of a wavefront are 64 threads, LDS is a shared array, a lane
-// exchange is a store / barrier / load / barrier, and the wave barrier is a
-// std::barrier.  The butterflies run the same pairwise operations as the device
-// shuffles.  Never part of the product library.
+// host: the 64 lanes of a wavefront are 64 cooperative fibers (ucontext) on one thread,
+// LDS is a shared array, a lane exchange is a store / barrier / load / barrier, and the
+// wave barrier passes control round-robin to the next lane (lane 0 resumes once lane 63
+// has arrived: every lane calls the same barriers, as on the device).  Problems run in
+// parallel, one OS thread each (MPCG_HOST_THREADS, default the machine's CPUs).  With
+// -DHOST_OS_THREADS the lanes are 64 OS threads and a std::barrier instead (slow under
+// oversubscription: a futex round per barrier).  The butterflies run the same pairwise
+// operations as the device shuffles.  Never part of the product library.
 //
 // stdin:  N dt ref_cte ref_eth ref_v w_cte w_eth w_v w_w w_a w_dw w_da max_w max_a bound tol max_iter
 //         model lf
@@ -17,15 +21,89 @@
 // stdout: per problem: status iters obj u0[2] traj[3N] restoration-phases filter-overflows filter-peak
 #include <barrier>
 #include <type_traits>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
+#include <ucontext.h>
+#ifdef __SANITIZE_ADDRESS__
+#include <sanitizer/common_interface_defs.h>
+#endif
+
 #include "../../mpc_ros_amd/csrc/wide_core.h"
 
+// 64 lanes as fibers on the calling thread: wait() hands control to the next lane in
+// round-robin order, so a lane resumes after every other lane has reached the same barrier
+struct Fibers {
+    static constexpr size_t kStack = 4u << 20;  // (lazily committed)
+    ucontext_t main_ctx, ctx[64];
+    std::unique_ptr<char[]> stack[64];
+    int ndone = 0;
+    void* fn = nullptr;  // the lane body: void(int lane)
+    void (*call)(void*, int) = nullptr;
+#ifdef __SANITIZE_ADDRESS__
+    void* fake = nullptr;
+#endif
+    void swap_to(ucontext_t* from, int to_lane) {
+#ifdef __SANITIZE_ADDRESS__
+        __sanitizer_start_switch_fiber(&fake, stack[to_lane].get(), kStack);
+#endif
+        swapcontext(from, &ctx[to_lane]);
+#ifdef __SANITIZE_ADDRESS__
+        __sanitizer_finish_switch_fiber(fake, nullptr, nullptr);
+#endif
+    }
+    void wait(int t) { swap_to(&ctx[t], (t + 1) & 63); }
+    static void entry(int hi, int lo, int t) {
+        Fibers* f = (Fibers*)(((uintptr_t)(unsigned)hi << 32) | (uintptr_t)(unsigned)lo);
+#ifdef __SANITIZE_ADDRESS__
+        __sanitizer_finish_switch_fiber(f->fake, nullptr, nullptr);
+#endif
+        f->call(f->fn, t);
+        // a finished lane passes on; the last one returns to the caller
+        if (++f->ndone == 64) {
+#ifdef __SANITIZE_ADDRESS__
+            __sanitizer_start_switch_fiber(nullptr, nullptr, 0);
+#endif
+            setcontext(&f->main_ctx);
+        }
+        f->swap_to(&f->ctx[t], (t + 1) & 63);
+    }
+    template <class F>
+    void run(F& body) {
+        fn = &body;
+        call = [](void* b, int t) { (*(F*)b)(t); };
+        const uintptr_t me = (uintptr_t)this;
+        for (int t = 0; t < 64; ++t) {
+            if (!stack[t]) stack[t].reset(new char[kStack]);
+            getcontext(&ctx[t]);
+            ctx[t].uc_stack.ss_sp = stack[t].get();
+            ctx[t].uc_stack.ss_size = kStack;
+            ctx[t].uc_link = nullptr;
+            makecontext(&ctx[t], (void (*)())entry, 3, (int)(me >> 32), (int)(me & 0xffffffffu), t);
+        }
+        ndone = 0;
+#ifdef __SANITIZE_ADDRESS__
+        __sanitizer_start_switch_fiber(&fake, stack[0].get(), kStack);
+#endif
+        swapcontext(&main_ctx, &ctx[0]);
+#ifdef __SANITIZE_ADDRESS__
+        __sanitizer_finish_switch_fiber(fake, nullptr, nullptr);
+#endif
+    }
+};
+
 struct HostShared {
+#ifdef HOST_OS_THREADS
     std::barrier<> bar{64};
+#else
+    Fibers* fib = nullptr;
+#endif
     double xd[64];
     int xi[64];
     std::vector<double> lds;
@@ -43,7 +121,11 @@ struct HostWave {
     double* S() const { return lds; }
     template <class U>
     U* Sp() const { return reinterpret_cast<U*>(lds); }
+#ifdef HOST_OS_THREADS
     void sync() const { sh->bar.arrive_and_wait(); }
+#else
+    void sync() const { sh->fib->wait(t); }
+#endif
     void gsync() const { sync(); }
     template <class U>
     U from(U v, int src) const {
@@ -163,10 +245,15 @@ int main() {
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
     const mpcg::WideLayout L(P.N, P.filter_cap, P.model);
+    std::vector<mpcg::IpmProblem<HT>> probs(B);
     for (long b = 0; b < B; ++b) {
-        mpcg::IpmProblem<HT> pr;
-        for (HT& v : pr.init) { double d; std::scanf("%lf", &d); v = (HT)d; }
-        for (HT& v : pr.c) { double d; std::scanf("%lf", &d); v = (HT)d; }
+        for (HT& v : probs[b].init) { double d; std::scanf("%lf", &d); v = (HT)d; }
+        for (HT& v : probs[b].c) { double d; std::scanf("%lf", &d); v = (HT)d; }
+    }
+    std::vector<std::string> out(B);
+    // one problem: its 64 lanes, then its output line
+    auto solve_one = [&](long b, void* fibers) {
+        const mpcg::IpmProblem<HT> pr = probs[b];
         HostShared sh;
         sh.lds.assign(L.total(), std::nan(""));
         std::vector<HT> spill(L.slot(), (HT)std::nan(""));
@@ -174,62 +261,94 @@ int main() {
         int status = 0, iters = 0, nresto = 0, nfover = 0, nfpeak = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
-        std::vector<std::thread> th;
-        for (int t = 0; t < 64; ++t) {
-            th.emplace_back([&, t]() {
-                HostWave wv{&sh, t, sh.lds.data()};
-                auto run = [&](auto& S0) {
-                    typedef std::decay_t<decltype(S0)> Solver;
-                    S0.solve();
-                    // a restoration phase: parked and continued as the device's second kernel does
-                    Solver S2(P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
-                    const bool parked = S0.status == Solver::NEED_RESTO;
-                    if (parked) {
-                        S0.park(park.data());
-                        sh.bar.arrive_and_wait();
-                        S2.unpark(park.data());
-                        S2.finish_resto();
-                    }
-                    Solver& S = parked ? S2 : S0;
-                    const double o = S.objective_out();
-                    if (t == 0) {
-                        status = S.status;
-                        iters = S.iter;
-                        nresto = S.n_resto;
-                        nfover = S.n_fover;
-                        nfpeak = S.nf_peak;
-                        obj = o;
-                        u0 = S.x_ctrl(0, 0);
-                        u1 = S.x_ctrl(1, 0);
-                        for (int s = 0; s < 3; ++s)
-                            for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
-                    }
-                };
-                if (P.model == 1 && P.N > 64) {
-                    mpcg::WideSolver<HostWave, 1, false, HT, 2> S(P, pr, wv, spill.data());
-                    run(S);
-                } else if (P.model == 0 && P.N > 64) {
-                    mpcg::WideSolver<HostWave, 0, false, HT, 2> S(P, pr, wv, spill.data());
-                    run(S);
-                } else if (P.model == 1 && P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 1, true, HT> S(P, pr, wv, spill.data());
-                    run(S);
-                } else if (P.model == 1) {
-                    mpcg::WideSolver<HostWave, 1, false, HT> S(P, pr, wv, spill.data());
-                    run(S);
-                } else if (P.N <= 32) {
-                    mpcg::WideSolver<HostWave, 0, true, HT> S(P, pr, wv, spill.data());
-                    run(S);
-                } else {
-                    mpcg::WideSolver<HostWave, 0, false, HT> S(P, pr, wv, spill.data());
-                    run(S);
+        auto lane = [&](int t) {
+            HostWave wv{&sh, t, sh.lds.data()};
+            auto run = [&](auto& S0) {
+                typedef std::decay_t<decltype(S0)> Solver;
+                S0.solve();
+                // a restoration phase: parked and continued as the device's second kernel does
+                Solver S2(P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
+                const bool parked = S0.status == Solver::NEED_RESTO;
+                if (parked) {
+                    S0.park(park.data());
+                    wv.sync();
+                    S2.unpark(park.data());
+                    S2.finish_resto();
                 }
-            });
-        }
+                Solver& S = parked ? S2 : S0;
+                const double o = S.objective_out();
+                if (t == 0) {
+                    status = S.status;
+                    iters = S.iter;
+                    nresto = S.n_resto;
+                    nfover = S.n_fover;
+                    nfpeak = S.nf_peak;
+                    obj = o;
+                    u0 = S.x_ctrl(0, 0);
+                    u1 = S.x_ctrl(1, 0);
+                    for (int s = 0; s < 3; ++s)
+                        for (int k = 0; k < P.N; ++k) traj[s * P.N + k] = S.x_state(s, k);
+                }
+            };
+            if (P.model == 1 && P.N > 64) {
+                mpcg::WideSolver<HostWave, 1, false, HT, 2> S(P, pr, wv, spill.data());
+                run(S);
+            } else if (P.model == 0 && P.N > 64) {
+                mpcg::WideSolver<HostWave, 0, false, HT, 2> S(P, pr, wv, spill.data());
+                run(S);
+            } else if (P.model == 1 && P.N <= 32) {
+                mpcg::WideSolver<HostWave, 1, true, HT> S(P, pr, wv, spill.data());
+                run(S);
+            } else if (P.model == 1) {
+                mpcg::WideSolver<HostWave, 1, false, HT> S(P, pr, wv, spill.data());
+                run(S);
+            } else if (P.N <= 32) {
+                mpcg::WideSolver<HostWave, 0, true, HT> S(P, pr, wv, spill.data());
+                run(S);
+            } else {
+                mpcg::WideSolver<HostWave, 0, false, HT> S(P, pr, wv, spill.data());
+                run(S);
+            }
+        };
+#ifdef HOST_OS_THREADS
+        (void)fibers;
+        std::vector<std::thread> th;
+        for (int t = 0; t < 64; ++t) th.emplace_back(lane, t);
         for (auto& x : th) x.join();
-        std::printf("%d %d %.17g %.17g %.17g", status, iters, obj, u0, u1);
-        for (double v : traj) std::printf(" %.17g", v);
-        std::printf(" %d %d %d\n", nresto, nfover, nfpeak);
-    }
+#else
+        sh.fib = (Fibers*)fibers;
+        sh.fib->run(lane);
+#endif
+        std::string line;
+        char buf[64];
+        std::snprintf(buf, sizeof buf, "%d %d %.17g %.17g %.17g", status, iters, obj, u0, u1);
+        line += buf;
+        for (double v : traj) {
+            std::snprintf(buf, sizeof buf, " %.17g", v);
+            line += buf;
+        }
+        std::snprintf(buf, sizeof buf, " %d %d %d\n", nresto, nfover, nfpeak);
+        line += buf;
+        out[b] = line;
+    };
+    // problems in parallel: one OS thread each, taking the next problem
+#ifdef HOST_OS_THREADS
+    int nth = 1;  // (64 OS threads per problem already)
+#else
+    const char* env = std::getenv("MPCG_HOST_THREADS");
+    int nth = env ? std::atoi(env) : (int)std::thread::hardware_concurrency();
+    nth = nth < 1 ? 1 : nth;
+#endif
+    if (nth > B) nth = (int)(B > 0 ? B : 1);
+    std::atomic<long> next{0};
+    auto worker = [&]() {
+        auto fib = std::make_unique<Fibers>();
+        for (long b; (b = next.fetch_add(1)) < B;) solve_one(b, fib.get());
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nth; ++i) pool.emplace_back(worker);
+    worker();
+    for (auto& x : pool) x.join();
+    for (long b = 0; b < B; ++b) std::fputs(out[b].c_str(), stdout);
     return 0;
 }
