@@ -119,17 +119,21 @@ WideInst wide_kernel(const IpmParams& P, int64_t B) {
         return nb == 2 ? SK(0, false, float, 2, false, 2)
              : split ? SK(0, true, float, 1, false, 3) : SK(0, false, float, 1, false, 3);
     const bool one = wide_lds_bytes(P) > 32768;
+    // (default Ipopt options: the instances that compile them as constants -- the benchmark
+    // configuration, configs[4]'s bicycle and the unsplit horizons of 33..64 stages at two
+    // wavefronts per SIMD)
+    const bool dflt = ipopt_options_are_default(P);
     if (P.model == 1)
         return nb == 2 ? SK(1, false, double, 2, false, 1)
-             : split ? SK(1, true, double, 1, false, 2)
+             : split ? (dflt ? SK(1, true, double, 1, true, 2) : SK(1, true, double, 1, false, 2))
              : one   ? SK(1, false, double, 1, false, 1)
                      : SK(1, false, double, 1, false, 2);
-    if (split && ipopt_options_are_default(P))  // (the benchmark configuration)
+    if (split && dflt)  // (the benchmark configuration)
         return B <= kLoneBatch ? SK(0, true, double, 1, true, 1) : SK(0, true, double, 1, true, 2);
     return nb == 2 ? SK(0, false, double, 2, false, 1)
          : split ? SK(0, true, double, 1, false, 2)
          : one   ? SK(0, false, double, 1, false, 1)
-                 : SK(0, false, double, 1, false, 2);
+                 : (dflt ? SK(0, false, double, 1, true, 2) : SK(0, false, double, 1, false, 2));
 }
 
 // XCDs of the current device (HW_REG_XCC_ID partitions of the workspace slots); 8 on an

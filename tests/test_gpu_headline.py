@@ -111,7 +111,7 @@ def test_bicycle_instance_at_large_batch(torch_cuda, bicycle_golden, features_go
     S, C, pos, rest = _padded(st, cf, B_BIG, 5, 3_000_000)
     s = _solver(g["P"])
     r = s.solve(S, C)
-    assert s.last_kernel == "k_solve_wide<1,true,double,1,false,2>"
+    assert s.last_kernel == "k_solve_wide<1,true,double,1,true,2>"
     check_against(_sub(r, pos), exp)
     sample = rest[:: len(rest) // 256][:256]
     check_against(_sub(r, sample), oracle_ref(oracle, g["P"], S[sample], C[sample]))
