@@ -120,19 +120,19 @@ WideInst wide_kernel(const IpmParams& P, int64_t B) {
              : split ? SK(0, true, float, 1, false, 3) : SK(0, false, float, 1, false, 3);
     const bool one = wide_lds_bytes(P) > 32768;
     // (default Ipopt options: the instances that compile them as constants -- the benchmark
-    // configuration, configs[4]'s bicycle and the unsplit horizons of 33..64 stages at two
-    // wavefronts per SIMD)
+    // configuration, configs[4]'s bicycle, and every fp64 horizon of the differential drive
+    // and the bicycle's 33..64 stages at two wavefronts per SIMD)
     const bool dflt = ipopt_options_are_default(P);
     if (P.model == 1)
         return nb == 2 ? SK(1, false, double, 2, false, 1)
              : split ? (dflt ? SK(1, true, double, 1, true, 2) : SK(1, true, double, 1, false, 2))
              : one   ? SK(1, false, double, 1, false, 1)
-                     : SK(1, false, double, 1, false, 2);
+                     : (dflt ? SK(1, false, double, 1, true, 2) : SK(1, false, double, 1, false, 2));
     if (split && dflt)  // (the benchmark configuration)
         return B <= kLoneBatch ? SK(0, true, double, 1, true, 1) : SK(0, true, double, 1, true, 2);
-    return nb == 2 ? SK(0, false, double, 2, false, 1)
+    return nb == 2 ? (dflt ? SK(0, false, double, 2, true, 1) : SK(0, false, double, 2, false, 1))
          : split ? SK(0, true, double, 1, false, 2)
-         : one   ? SK(0, false, double, 1, false, 1)
+         : one   ? (dflt ? SK(0, false, double, 1, true, 1) : SK(0, false, double, 1, false, 1))
                  : (dflt ? SK(0, false, double, 1, true, 2) : SK(0, false, double, 1, false, 2));
 }
 

@@ -379,12 +379,15 @@ const void* resume_kernel_fn();
     X(2, 0, false, double, 1, false, 1)       \
     X(5, 0, false, double, 1, true, 2)        \
     X(3, 0, false, double, 2, false, 1)       \
+    X(1, 0, false, double, 2, true, 1)        \
+    X(6, 0, false, double, 1, true, 1)        \
     X(4, 0, true, float, 1, false, 3)         \
     X(5, 0, false, float, 1, false, 3)        \
     X(6, 0, false, float, 2, false, 2)        \
     X(7, 1, true, double, 1, false, 2)        \
     X(4, 1, true, double, 1, true, 2)         \
     X(8, 1, false, double, 1, false, 2)       \
+    X(7, 1, false, double, 1, true, 2)        \
     X(8, 1, false, double, 1, false, 1)       \
     X(9, 1, false, double, 2, false, 1)
 // (the fp32 solver's problems that need the restoration phase are solved again in fp64: its
