@@ -401,3 +401,36 @@ def test_default_option_instance_equals_general(torch_cuda, features_golden, ora
     o.watchdog_shortened_iter_trigger = 0
     ref = oracle.mpc_solve_batch(g["P"], g["state"], g["coeffs"], opts=o, nthreads=8, diag=True)
     check_against(c, ref, min_same_iters=1.0)
+
+
+@pytest.mark.parametrize("name", ["N40", "N64", "bicycle", "bicycle_N40"])
+def test_default_option_instances_equal_general(torch_cuda, features_golden, variants_golden, bicycle_golden,
+                                                oracle, name):
+    """Every other fp64 configuration's default-options instance (N = 33..64 at two
+    wavefronts per SIMD, N = 64's one-wavefront instance, configs[4]'s bicycle, the bicycle
+    at N = 40) against the general instance bitwise -- fixture rows (restoration, SOC and
+    watchdog rows included) and the oracle on the same rows."""
+    from mpc_ros_amd import infinity, params
+
+    if name == "N40":
+        g = variants_golden["N40"]
+        P, st, cf = params_from_array(g["params"]), g["state"], g["coeffs"]
+        f = features_golden["resto_N40"]
+        st, cf = np.concatenate([st, f["state"]]), np.concatenate([cf, f["coeffs"]])
+    elif name == "bicycle":
+        g, f = bicycle_golden, features_golden["bicycle"]
+        P, st, cf = g["P"], np.concatenate([g["state"], f["state"]]), np.concatenate([g["coeffs"], f["coeffs"]])
+    else:
+        P = dict(params.PLUGIN_DEFAULTS, STEPS=64 if name == "N64" else 40)
+        if name == "bicycle_N40":
+            P.update(MODEL=1, LF=0.5, ANGVEL=0.5)
+        st, cf = infinity.make_problems(np.arange(7000, 7032))
+    sa, sb = solver_for(P), solver_for(P, acceptable_obj_change_tol=1e30)
+    a, b = sa.solve(st, cf), sb.solve(st, cf)
+    # (k_solve_wide<model,split,type,blocks,default options,waves per SIMD>: only the fifth differs)
+    ka, kb = sa.last_kernel[:-1].split(","), sb.last_kernel[:-1].split(",")
+    assert ka[4] == "true" and kb[4] == "false" and ka[:4] + ka[5:] == kb[:4] + kb[5:], (ka, kb)
+    for k in ("u0", "traj", "status", "iters", "obj"):
+        np.testing.assert_array_equal(a[k], b[k])
+    ref = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ref_opts(int(P["STEPS"])), nthreads=16, diag=True)
+    check_against(a, ref)
