@@ -108,13 +108,19 @@ typedef struct mpcg_params {
     /* Arithmetic of the solve: 0 = fp64 (the reference's double, the default); 1 = fp32
      * (BASELINE configs[2]; differential drive only): iterate, multipliers and Newton systems
      * in float -- state a tolerance a float iterate can meet (tol ~1e-5 instead of 1e-8;
-     * tiny_step_tol 10 FLT_EPSILON).  Inputs and outputs stay double. */
+     * tiny_step_tol 10 FLT_EPSILON).  Inputs and outputs stay double.
+     * Escalation (precision 1, no_restoration 0): a problem the fp32 solver cannot finish --
+     * its line search fails where Ipopt would enter the restoration phase, it would end with
+     * 9 (restoration failure), 3 (tiny step) or 2 (max_iter) -- is solved again from the
+     * start by the fp64 solver with the reference's Ipopt options (the 3.12 defaults of the
+     * fields above; only max_cpu_time and the problem parameters are kept from these params).
+     * Such a row reports the fp64 solve: its status, and iters counting only the fp64
+     * iterations; diag[:, 2] = 3 marks it. */
     int32_t precision;
-    /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails; 1:
-     * stop there with RESTORATION_FAILURE (9) instead.  The fp32 solver's setting (its line
-     * search fails at a float iterate's noise floor, where the restoration phase costs a
-     * long lone-wavefront tail and rarely ends in success).  Occupies the struct's padding:
-     * sizeof(mpcg_params) is unchanged. */
+    /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails (fp32:
+     * the escalation above); 1: stop there with RESTORATION_FAILURE (9) instead, and no fp32
+     * escalation (the fp32 ending is kept).  Occupies the struct's padding: sizeof(mpcg_params)
+     * is unchanged. */
     int32_t no_restoration;
 } mpcg_params;
 
@@ -149,15 +155,23 @@ int mpcg_get_params(const mpcg_handle* h, mpcg_params* p);
  * area can overflow), and the solve-order buffers (B > 2048); reserve it ahead of graph
  * capture (a solve that must grow it allocates and synchronises the device). */
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B);
+/* The same for a handle: its parameters, its park capacity (mpcg_set_park_capacity) and the XCD
+ * count of its device (the slot partitions) -- what mpcg_reserve(h, B) allocates. */
+size_t mpcg_handle_workspace_bytes(const mpcg_handle* h, int64_t B);
 int mpcg_reserve(mpcg_handle* h, int64_t B);
 /* Park-area entries of the handle's solves (0 = the default max(256, B/128)).  A problem that
  * enters the restoration phase while every entry is taken goes to an overflow list and is
  * solved again from the start after the batch (the same iterates, diag[:, 2] = 2): results do
- * not depend on the capacity, only the tail does.  A tuning and test knob. */
+ * not depend on the capacity, only the tail does.  A tuning and test knob.  Set it before
+ * mpcg_reserve: a larger capacity grows the workspace, and the next solve would otherwise
+ * allocate it (with a device synchronisation -- not during graph capture). */
 int mpcg_set_park_capacity(mpcg_handle* h, int64_t cap);
 /* The solver kernel instance the handle's last solve launched, "k_solve_wide<model, split,
  * type, stage blocks, default options, waves per SIMD>" ("" before the first solve). */
 const char* mpcg_last_kernel(const mpcg_handle* h);
+/* 1 if the handle's last solve ran its problems in expected-longest-first order (batches of
+ * B > 2048: a radix sort of the path curvature before the batch kernel), 0 otherwise. */
+int mpcg_last_solve_order(const mpcg_handle* h);
 
 /* Batched solve, host buffers, synchronous (copies in, solves, copies out).
  *   state  [B][6]  x, y, theta, v, cte, etheta   (MPC::Solve `state`)
@@ -180,7 +194,8 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
  * may be NULL): restoration phases entered, filter entries dropped beyond its capacity
  * (filter_cap in LDS plus 448 in the workspace; Ipopt's filter is unbounded, so any nonzero
  * value marks a solve that may differ from Ipopt's), 1 if the problem was continued by the
- * parked-problem kernel (2 if it was solved again after a park-area overflow, 0 otherwise), the
+ * parked-problem kernel (2 if it was solved again after a park-area overflow, 3 if an fp32
+ * problem was solved again in fp64 -- the escalation under `precision` -- 0 otherwise), the
  * most filter entries held at once (the original problem). */
 int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
                   int32_t* status, double* obj, int32_t* iters, int32_t* diag);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "mpcg_set_params": ([C.c_void_p, _PP], C.c_int),
     "mpcg_get_params": ([C.c_void_p, _PP], C.c_int),
     "mpcg_workspace_bytes": ([_PP, C.c_int64], C.c_size_t),
+    "mpcg_handle_workspace_bytes": ([C.c_void_p, C.c_int64], C.c_size_t),
     "mpcg_reserve": ([C.c_void_p, C.c_int64], C.c_int),
     "mpcg_solve": ([C.c_void_p, C.c_int64, _dp, _dp, _dp, _dp, _ip, _dp, _ip], C.c_int),
     "mpcg_solve_device": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -91,6 +92,7 @@ SIGNATURES = {
     "mpcg_get_strategy": ([C.c_void_p], C.c_int),
     "mpcg_set_park_capacity": ([C.c_void_p, C.c_int64], C.c_int),
     "mpcg_last_kernel": ([C.c_void_p], C.c_char_p),
+    "mpcg_last_solve_order": ([C.c_void_p], C.c_int),
     "mpcg_synth_infinity_device": ([C.c_void_p, C.c_uint64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p], C.c_int),
 }

@@ -79,6 +79,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
              "-Wno-unused-result", "-Wno-unused-value",
              f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"',
              "-Rpass-analysis=kernel-resource-usage"]
+    # (diagnostic builds only: extra compiler flags, e.g. -DMPCG_DEBUG_GUARD)
+    flags += os.environ.get("MPCG_EXTRA_CFLAGS", "").split()
     tmp = tempfile.mkdtemp(prefix="mpcg_build_")
     try:
         def cc(unit):
@@ -114,7 +116,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     return LIB
 
 
-RESOURCES = os.path.join(ROOT, "profiles", "r4", "resources.json")
+RESOURCES = os.path.join(ROOT, "profiles", "r5", "resources.json")
 
 
 def demangle(names):

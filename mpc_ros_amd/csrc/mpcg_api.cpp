@@ -62,6 +62,8 @@ struct mpcg_handle {
     bool have_last = false;
     // the solver kernel instance the last solve launched (mpcg_last_kernel)
     const char* last_kernel = "";
+    // 1 if the last solve ran in expected-longest-first order (B > kOrderMinBatch)
+    int last_ordered = 0;
     // park-area entries (0: the default, max(256, B / 128))
     int64_t park_cap = 0;
     // the synthetic robots' arc-length table (mpcg_synth_infinity_device), uploaded once
@@ -279,11 +281,24 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
 
 // solve-order buffers (batches beyond the resident wavefronts)
 static const int64_t kOrderMinBatch = 2048;
+static mpcg::IpmParams handle_ipm(const mpcg_handle* h);
 
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B) {
     if (!p || B <= 0) return 0;
     const mpcg::IpmParams P = to_ipm(*p);
     return mpcg::wide_spill_bytes(P, B) + (B > kOrderMinBatch ? mpcg::wide_sched_bytes(B) : 0);
+}
+
+// (the handle's own: its parameters, park capacity and device -- the slot partitions follow the
+// device's XCD count)
+size_t mpcg_handle_workspace_bytes(const mpcg_handle* h, int64_t B) {
+    if (!h || B <= 0) return 0;
+    int prev = -1;
+    const bool sw = hipGetDevice(&prev) == hipSuccess && prev != h->device;
+    if (sw && hipSetDevice(h->device) != hipSuccess) return 0;
+    const size_t n = mpcg::wide_spill_bytes(handle_ipm(h), B) + (B > kOrderMinBatch ? mpcg::wide_sched_bytes(B) : 0);
+    if (sw) hipSetDevice(prev);
+    return n;
 }
 
 int mpcg_create(int device, mpcg_handle** out) {
@@ -473,6 +488,7 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
                                 (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join,
                                 &h->last_kernel);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
+    h->last_ordered = order != nullptr;
     return record_on(h, s);
 }
 
@@ -606,6 +622,7 @@ int mpcg_track_device(mpcg_handle* h, int64_t B, int32_t M, const double* d_pose
 }
 
 const char* mpcg_last_kernel(const mpcg_handle* h) { return h ? h->last_kernel : ""; }
+int mpcg_last_solve_order(const mpcg_handle* h) { return h ? h->last_ordered : 0; }
 
 int mpcg_synth_infinity_device(mpcg_handle* h, uint64_t seed, int64_t start, int64_t B, int32_t M, double* d_pose,
                                double* d_vel, double* d_plan, void* stream) {

@@ -233,8 +233,8 @@ int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double
     }
     // the gather: rank r > 0 sends each of its output arrays, the root receives them at their
     // offsets (grouped point-to-point: every shard moves once over xGMI).  The plan is checked
-    // before the group opens; a failing call inside it aborts the communicators (ncclGroupEnd
-    // would otherwise launch an unmatched send that a stream then waits for).
+    // before the group opens; a failing call inside it closes the group (not launched: it has a
+    // recorded error) and then aborts the communicators, so no unmatched send is waited for.
     std::vector<mpcg_xfer> plan((size_t)ngpu * MPCG_GATHER_ARRAYS);
     for (int r = 1; r < ngpu; ++r)
         if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, &plan[(size_t)r * MPCG_GATHER_ARRAYS])) != 0) return rc;
@@ -253,9 +253,11 @@ int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double
         }
     }
     if (grc) {
+        // close the group first (it still holds the communicators; a group with a recorded
+        // error is not launched), then abort them
         m->broken = true;
-        for (auto& c : m->comms) ncclCommAbort(c), c = nullptr;
         ncclGroupEnd();
+        for (auto& c : m->comms) ncclCommAbort(c), c = nullptr;
         return grc;
     }
     if ((ne = ncclGroupEnd()) != ncclSuccess) {

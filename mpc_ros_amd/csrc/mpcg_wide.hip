@@ -148,9 +148,9 @@ int device_xccs() {
 
 // Workspace slots for a batch of B: four times the wavefronts the device can hold resident at
 // once (occupancy of the instance at its LDS size times the CUs), at most B (at least 32 per
-// XCD), in one equal partition per XCD (device_xccs).  A wavefront claims slot blockIdx mod the partition size
-// in its XCD's partition, or the next free one: with the margin, a slow problem still
-// holding a slot rarely makes a later wavefront probe further.
+// XCD), in one equal partition per XCD (device_xccs).  A wavefront takes the slot its XCD
+// released last (claim_slot: a LIFO stack per partition), so the slots in use stay L2-warm;
+// the margin covers uneven dispatch over the XCDs.
 int64_t wide_slots(const IpmParams& P, int64_t B) {
     if (B <= 0) return 0;
     int64_t n = 4096;  // (fallback if the runtime cannot say)
@@ -254,8 +254,9 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // the workspace (wide_spill_bytes): slot flags | counters: park count, taken, done,
-    // started, overflow count, overflow taken (256 B) | park indices | park ready flags |
+    // the workspace (wide_spill_bytes): slot links | counters: park count, taken, done,
+    // started, overflow count, overflow taken (bytes 0..23), the slot stacks' heads (64..191,
+    // one 8-byte head per XCD) and fresh counters (192..255) | park indices | park ready flags |
     // overflow list | slots | park area
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     if (ns < 1 || wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
@@ -273,16 +274,18 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     void* slots = w;
     w += (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns;
     void* park = w;
-    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot flags, counters)
+    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot links, counters, empty stacks)
     if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
     if (e == hipSuccess && ovf_bytes(P, B)) e = hipMemsetAsync(ovf, 0xFF, ovf_bytes(P, B), stream);  // (all -1)
     if (e != hipSuccess) return e;
     const bool esc = escalates(P);
     // (the fp32 solver's batch parks nothing: every problem that needs the restoration phase
     // goes to the overflow list)
+    const int nxcc = device_xccs();
     WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
+               (unsigned long long*)(cnt + 16), cnt + 48,
                (int32_t)ns, (int32_t)slot_elems(P), cnt, esc ? 0 : (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
-               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0, 0, 2};
+               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)nxcc, 0, 0, 2};
     void* args[] = {(void*)&a};
     // the resume workers' arguments: the fp32 solver's escalations run the fp64 solver
     const IpmParams Pr = esc ? fp64_params(P) : P;
@@ -305,9 +308,16 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     // stream continues after both (no host synchronisation).  Under graph capture the two
     // branches need not run concurrently: the workers then exit at once (take_parked) and
     // the drain takes every parked problem.
-    const bool fork = aux && aux != stream && ev_fork && ev_join;
+    // (escalations: at most pc - 1 concurrent workers, so the drain after the batch kernel always
+    // has an entry of its own -- the concurrent workers exit after ~2 ms when the batch kernel
+    // has not started, e.g. a graph executor that serialises the fork, and the overflow list
+    // must still be taken.  No worker, no fork: a captured fork whose branch holds no work
+    // deadlocked the second replay of the graph.)
     const int64_t nw = esc ? escalation_workers(B) : resume_workers(B);
-    const unsigned workers = fork ? (unsigned)(pc < nw ? pc : nw) : 0u;
+    const int64_t wmax = esc ? pc - 1 : pc;
+    const bool can_fork = aux && aux != stream && ev_fork && ev_join;
+    const unsigned workers = can_fork ? (unsigned)(wmax < nw ? wmax : nw) : 0u;
+    const bool fork = workers > 0;
     if (fork) {
         e = hipEventRecord(ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);

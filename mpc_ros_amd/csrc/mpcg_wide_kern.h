@@ -31,7 +31,12 @@ struct WideArgs {
     int32_t* iters;
     int32_t* diag;         // [B][4] restoration phases, filter overflows, parked (1) / re-solved (2), filter peak (or null)
     void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
-    int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
+    // the free slots of each XCD's partition: a LIFO stack (claim_slot / release_slot) --
+    // slot_next[s] the slot below s, slot_head[x] (tag << 32 | top + 1) the top of XCD x's
+    // stack, slot_fresh[x] the slots of the partition not yet handed out
+    int32_t* slot_next;
+    unsigned long long* slot_head;
+    int32_t* slot_fresh;
     int32_t nslots;        // nxcc partitions of nslots / nxcc slots, one per XCD
     int32_t slot_elems;    // WideLayout::spill() rounded up to whole 128-byte lines
     // parked problems (the restoration phase, continued by k_resume_wide while the batch
@@ -76,38 +81,67 @@ __device__ __forceinline__ int xcc_id(int nxcc) {
     return (int)(v & 15) % nxcc;
 }
 
-// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on:
-// the first free one from blockIdx on (a partition holds 4x the wavefronts an XCD keeps
-// resident, so the first probe normally succeeds; with fewer, a wavefront waits for a
-// resident one on its XCD to finish and release its slot).  A slot is therefore only ever
-// touched through one XCD's L2, so handing it over needs no agent-scope fence (an agent
-// release is a write-back of the whole XCD L2, buffer_wbl2, per wavefront: 1.6 GB of write
-// traffic per B = 65,536 launch when it was there).  The hand-over is ordered within the
-// XCD: release_slot waits for the owner's stores to complete (they are in the XCD's L2
-// then; the vector L1 is write-through) before the flag is cleared, and claim_slot
-// invalidates the claiming CU's vector L1 after the flag is taken, so no line a previous
-// owner wrote through another CU is read stale.  Slot lines are whole 128-byte lines, so two
-// XCDs never share one.  Vector atomics (device scope) on the flags.
-__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int nxcc, int64_t hint) {
-    const int per = nslots / nxcc, base = xcc_id(nxcc) * per;
-    int s = (int)(hint % per);
+// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on.  The
+// free slots of a partition form a LIFO stack (Treiber: 64-bit head = ABA tag << 32 | top + 1,
+// the link of each slot in slot_next; slots never handed out are taken from a counter when the
+// stack is empty), so a new problem takes the slot its XCD released last -- its lines are still
+// in that XCD's L2 (dirty ones are overwritten there instead of being written back to HBM:
+// the working set is the resident wavefronts' slots, not the whole partition).  A partition
+// holds 4x the wavefronts an XCD keeps resident, so a claim never waits in practice; with fewer,
+// a wavefront waits for a resident one on its XCD to release its slot.  A slot is only ever
+// touched through one XCD's L2, so handing it over needs no agent-scope fence (an agent release
+// is a write-back of the whole XCD L2, buffer_wbl2, per wavefront: 1.6 GB of write traffic per
+// B = 65,536 launch when it was there).  The hand-over is ordered within the XCD:
+// release_slot waits for the owner's stores to complete (they are in the XCD's L2 then; the
+// vector L1 is write-through) before it links the slot and publishes it (each atomic waited for
+// before the next), and claim_slot invalidates the claiming CU's vector L1 after taking it, so
+// no line a previous owner wrote through another CU is read stale.  Slot lines are whole
+// 128-byte lines, so two XCDs never share one.  Vector atomics, relaxed, on the L2.
+__device__ __forceinline__ int claim_slot(int32_t* next, unsigned long long* head, int32_t* fresh, int nslots,
+                                          int nxcc) {
+    const int x = xcc_id(nxcc), per = nslots / nxcc, base = x * per;
     int r = 0;
     if (threadIdx.x == 0) {
         for (;;) {
-            if (atomicCAS(&flags[base + s], 0, 1) == 0) break;
-            s = s + 1 == per ? 0 : s + 1;
-            if (s == (int)(hint % per)) __builtin_amdgcn_s_sleep(8);
+            const unsigned long long h = __hip_atomic_load(&head[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int top = (int)(h & 0xffffffffull) - 1;
+            if (top >= 0) {
+                const int below = __hip_atomic_load(&next[base + top], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long nh = (((h >> 32) + 1) << 32) | (unsigned long long)(uint32_t)(below + 1);
+                if (atomicCAS(&head[x], h, nh) == h) {
+                    r = base + top;
+                    break;
+                }
+                continue;
+            }
+            const int f = __hip_atomic_load(&fresh[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f < per) {
+                if (atomicCAS(&fresh[x], f, f + 1) == f) {
+                    r = base + f;
+                    break;
+                }
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(8);
         }
-        r = base + s;
     }
     r = __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");  // (acquire: the CU's L1)
     return r;
 }
-__device__ __forceinline__ void release_slot(int32_t* flags, int s) {
+__device__ __forceinline__ void release_slot(int32_t* next, unsigned long long* head, int nslots, int nxcc, int s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (release: the slot's stores are in L2)
     __builtin_amdgcn_wave_barrier();
-    if (threadIdx.x == 0) atomicExch(&flags[s], 0);
+    if (threadIdx.x == 0) {
+        const int per = nslots / nxcc, x = s / per;
+        for (;;) {
+            const unsigned long long h = __hip_atomic_load(&head[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicExch(&next[s], (int)(h & 0xffffffffull) - 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the link is in L2 before the slot is)
+            const unsigned long long nh = (((h >> 32) + 1) << 32) | (unsigned long long)(uint32_t)(s - x * per + 1);
+            if (atomicCAS(&head[x], h, nh) == h) break;
+        }
+    }
 }
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
@@ -141,7 +175,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
     if (blockIdx.x == 0 && t == 0) atomicExch(a.started, 1);
-    const int slot = claim_slot(a.slot_flags, a.nslots, a.nxcc, (int64_t)blockIdx.x);
+    int slot = claim_slot(a.slot_next, a.slot_head, a.slot_fresh, a.nslots, a.nxcc);
+#ifdef MPCG_DEBUG_GUARD
+    if (t == 0 && (a.B <= 4 || slot < 0 || slot >= a.nslots))
+        printf("solve blk %d p %ld slot %d nslots %d xcc %d\n", (int)blockIdx.x, (long)p, slot, a.nslots, xcc_id(a.nxcc));
+    if (slot < 0 || slot >= a.nslots) slot = 0;
+#endif
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     S.solve();
@@ -164,7 +203,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __builtin_amdgcn_wave_barrier();
             if (t == 0) atomicExch(&a.park_ready[e], 1);
-            release_slot(a.slot_flags, slot);
+            release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
             block_done(a.done);
             return;
         }
@@ -176,12 +215,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             const int o = atomicAdd(a.ovf_count, 1);
             atomicExch((unsigned long long*)&a.ovf_idx[o], (unsigned long long)p);
         }
-        release_slot(a.slot_flags, slot);
+        release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
         block_done(a.done);
         return;
     }
     write_out(a, S, p, 0);
-    release_slot(a.slot_flags, slot);
+    release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
     block_done(a.done);
 }
 
@@ -335,6 +374,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         } else {
             // the whole solve, in park entry ent0 + blockIdx.x (this worker's own)
             p = take_overflow(a);
+#ifdef MPCG_DEBUG_GUARD
+            if (threadIdx.x == 0)
+                printf("resume phase 1 blk %d ent0 %d p %ld B %ld ovf_count %d ovf_taken %d done %d\n", (int)blockIdx.x, a.ent0,
+                       (long)p, (long)a.B, *a.ovf_count, *a.ovf_taken, *a.done);
+            if (p >= a.B) return;
+#endif
             if (p < 0) return;
             ent = (T*)a.park + (int64_t)(a.ent0 + blockIdx.x) * a.park_stride;
         }

@@ -128,7 +128,12 @@ struct WideLayout {
     static constexpr int XMN = 84;   // ... their slack e = ds_k - z = N z + m, N = M - I (6x6) ...
     static constexpr int XMV = 120;  // ... m
     static constexpr int XE = 126;   // e of the last step (row form)
-    static constexpr int XS = 132;
+    // iterative refinement of the step (WideSolver::refine_resto): the full system's residual in
+    // the stage's x rows (8) and the rows' p, n, c rows (6 each) ...
+    static constexpr int XRX = 132, XRP = 140, XRN = 146, XRC = 152;
+    // ... and the step it refines: dx (8), dp, dn, y+ (6 each), the rows' right-hand side XCR (6)
+    static constexpr int XSX = 158, XSP = 166, XSN = 172, XSY = 178, XSC = 184;
+    static constexpr int XS = 190;
     static constexpr int XW = 72;   // spill copies: watchdog p n zp zn dp dn (0..35), SOC dp dn (36..47), soft p n zp zn (48..71)
     MPCG_HD int SP_DUMP() const { return spill(); }
     MPCG_HD int SP_EXT() const { return spill() + total(); }
@@ -263,6 +268,9 @@ struct WideSolver {
     // statistics of the restoration iterate: sum(p + n), ||D_R (x - x_R)||^2, and the original
     // problem's barrier function, violation and max violation at x
     T r_spn = 0, r_qx = 0, r_phiO = 0, r_thO = 0, r_pinfO = 0;
+    // a correction solve of the iterative refinement: the right-hand side is the residual in
+    // the records (XRX, XRP, XRN; XCR holds -r_c), not the barrier gradient (refine_resto)
+    bool rf_pass = false;
     // the monotone barrier update's loop state across a re-evaluation (k_rmu)
     T mu_Emu = 0;
     int mu_tf = 0;
@@ -2380,6 +2388,7 @@ struct WideSolver {
                 qd = eta * dr * dr + zl[j] * rdl + zu[j] * rdu + delta_w;
                 qv = eta * dr * dr * (w[j] - xR(k, j)) - mu * rdl + mu * rdu;
             }
+            if (rf_pass) qv = (j < 6 || !last) ? -xrec(k)[WideLayout::XRX + j] : (T)0;
             st(sb + WideLayout::SQD + j, qd);
             st(sb + WideLayout::SQV + j, qv);
         }
@@ -2393,7 +2402,11 @@ struct WideSolver {
             // (c_hat = c + r_p/sp - r_n/sn + D y = c + gphi_p/sp - gphi_n/sn: the y terms
             // cancel exactly, and are left out -- large where a row is active)
             (void)ys;
-            const T gp = (T)RHO - mu / p + (T)KD * mu, gn = (T)RHO - mu / n + (T)KD * mu;
+            T gp = (T)RHO - mu / p + (T)KD * mu, gn = (T)RHO - mu / n + (T)KD * mu;
+            if (rf_pass) {
+                gp = -x[WideLayout::XRP + j];
+                gn = -x[WideLayout::XRN + j];
+            }
             const T D = (T)1 / sp_ + (T)1 / sn_;
             const T ch = x[WideLayout::XCR + j] + gp / sp_ - gn / sn_;
             x[WideLayout::XDS + j] = (T)sqrt((double)(D / (rsc * rsc)));
@@ -2703,33 +2716,21 @@ struct WideSolver {
         wv.sync();
         T linp[NB][6];
         shift_blocks(lin, linp);
-        Fwd F{(T)1, (T)1, (T)0, (T)0};
         for (int b = 0; b < NB; ++b) {
             const int k = t + 64 * b;
             if (k >= N) continue;
-            const bool last = k == N - 1;
-            T w[8], zl[8], zu[8], gq[8], dk[8];
-            ldn<8>(L.W(k), w);
-            ldn<8>(L.ZL(k), zl);
-            ldn<8>(L.ZU(k), zu);
-            ldn<8>(L.ST(k) + WideLayout::SQV, gq);  // (the barrier gradient of x: precompute_resto)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) dk[q] = xs[b][q];
-            dk[6] = dus[b][0];
-            dk[7] = dus[b][1];
-            const int nv = last ? 6 : 8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < nv) dir_var(w[j], zl[j], zu[j], vlo(j), vhi(j), gq[j], dk[j], F);
             T* x = xrec(k);
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const T irs = rcp(rowscale(j, k));
-                const T ys = ld(L.Y(k) + j) * irs, dys = (ld(L.YP(k) + j) - ld(L.Y(k) + j)) * irs;
                 const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
                 const T zp = x[WideLayout::XZP + j], zn = x[WideLayout::XZN + j];
                 const T sp_ = zp / p + sv_delta, sn_ = zn / n + sv_delta;
-                const T gpp = (T)RHO - mu / p + (T)KD * mu, gpn = (T)RHO - mu / n + (T)KD * mu;
+                T gpp = (T)RHO - mu / p + (T)KD * mu, gpn = (T)RHO - mu / n + (T)KD * mu;
+                if (rf_pass) {
+                    gpp = -x[WideLayout::XRP + j];
+                    gpn = -x[WideLayout::XRN + j];
+                }
                 // the rows' steps: a variable whose Sigma dominates its unit coupling to the
                 // constraint row (the Bunch-Kaufman 1x1 pivot test, alpha = 0.6404) from its
                 // own row (dp = (y+ - gphi_p)/sp, dn = -(y+ + gphi_n)/sn), else from the
@@ -2746,9 +2747,48 @@ struct WideSolver {
                     dn = -(ysn + gpn) / sn_;
                     dp = sp_ >= bk ? (ysn - gpp) / sp_ : dn + q;
                 }
-                (void)ys;
                 x[WideLayout::XDP + j] = dp;
                 x[WideLayout::XDN + j] = dn;
+            }
+        }
+        wv.mark(5);
+        return Fwd{(T)1, (T)1, (T)0, (T)0};  // (the statistics: step_stats_resto, after the refinement)
+    }
+
+    // The step statistics of the restoration step in DW, XDP, XDN (fraction to the boundary,
+    // grad phi^T d, the relative step), after its iterative refinement; the barrier gradient of
+    // x as precompute_resto computes it.
+    MPCG_HD Fwd step_stats_resto() {
+        const int t = wv.lane();
+        wv.sync();
+        const T eta = eta_mu();
+        Fwd F{(T)1, (T)1, (T)0, (T)0};
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], zl[8], zu[8], dk[8];
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.ZL(k), zl);
+            ldn<8>(L.ZU(k), zu);
+            ldn<8>(L.DW(k), dk);
+            const int nv = last ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    const T dr = dR(k, j);
+                    const T rdl = (T)1 / (w[j] - vlo(j)), rdu = (T)1 / (vhi(j) - w[j]);
+                    const T gq = eta * dr * dr * (w[j] - xR(k, j)) - mu * rdl + mu * rdu;
+                    dir_var(w[j], zl[j], zu[j], vlo(j), vhi(j), gq, dk[j], F);
+                }
+            }
+            const T* x = xrec(k);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+                const T zp = x[WideLayout::XZP + j], zn = x[WideLayout::XZN + j];
+                const T gpp = (T)RHO - mu / p + (T)KD * mu, gpn = (T)RHO - mu / n + (T)KD * mu;
+                const T dp = x[WideLayout::XDP + j], dn = x[WideLayout::XDN + j];
                 dir_one(p, zp, gpp, dp, F);
                 dir_one(n, zn, gpn, dn, F);
             }
@@ -2760,9 +2800,222 @@ struct WideSolver {
         F.amax_z = v[1];
         F.gd = v[2];
         F.rel = v[3];
-        wv.mark(5);
         return F;
     }
+
+    // The residual of the full restoration system (z eliminated) at the step in DW, XDP, XDN and
+    // y+ in YP -- the x rows (H dx + J^T y+ = -grad phi_x), the p rows (Sigma_p dp - dy =
+    // -(grad phi_p - y)), the n rows (Sigma_n dn + dy = -(grad phi_n + y)) and the scaled
+    // constraint rows (J dx - dp + dn = -XCR) -- into the records (XRX, XRP, XRN, XRC), and
+    // Ipopt's residual ratio |r| / (min(|sol|, 1e6 |rhs|) + |rhs|) (max-norms;
+    // PDFullSpaceSolver::ComputeResidualRatio).
+    MPCG_HD T resid_resto() {
+        const int t = wv.lane();
+        wv.sync();
+        const T eta = eta_mu(), dlt = sv_delta;
+        T lin[NB][6], linp[NB][6];
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) lin[b][j] = 0;
+            if (k < N - 1) {
+                T a[8], dx[8], twl = dt, tvl = 0;
+                ldv<8>(L.ST(k) + WideLayout::SA, a);
+                ldn<8>(L.DW(k), dx);
+                if constexpr (MODEL == 1) ld2(L.ST(k) + WideLayout::STW, twl, tvl);
+                T l8[8];
+                A_mul(a, dx, l8);
+                if constexpr (MODEL == 1) {
+                    l8[2] += tvl * dx[3];
+                    l8[5] += tvl * dx[3];
+                }
+                l8[2] += twl * dx[6];
+                l8[3] += dt * dx[7];
+                l8[5] += twl * dx[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) lin[b][j] = l8[j];
+            }
+        }
+        shift_blocks(lin, linp);
+        T rn = 0, sn = 0, bn = 0;
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            const bool last = k == N - 1;
+            T w[8], dx[8], qd[8], a[8], cv[6], yp[6], y[6], ypn[6] = {0, 0, 0, 0, 0, 0}, yn[6] = {0, 0, 0, 0, 0, 0};
+            ldn<8>(L.W(k), w);
+            ldn<8>(L.DW(k), dx);
+            const int sb = L.ST(k);
+            ldv<8>(sb + WideLayout::SQD, qd);
+            ldv<8>(sb + WideLayout::SA, a);
+            ldv<6>(sb + WideLayout::SCV, cv);
+            ldn<6>(L.YP(k), yp);
+            ldn<6>(L.Y(k), y);
+            if (!last) {
+                ldn<6>(L.YP(k + 1), ypn);
+                ldn<6>(L.Y(k + 1), yn);
+            }
+            T twk = dt, tvk = 0, hvd = 0;
+            if constexpr (MODEL == 1) {
+                twk = ld(sb + WideLayout::STW);
+                tvk = ld(sb + WideLayout::STV);
+                hvd = ld(sb + WideLayout::SHVD);
+            }
+            T at[6] = {0, 0, 0, 0, 0, 0}, aty[6] = {0, 0, 0, 0, 0, 0};
+            if (!last) {
+                AT_mul(a, ypn, at);
+                AT_mul(a, yn, aty);
+                if constexpr (MODEL == 1) {
+                    at[3] += tvk * (ypn[2] + ypn[5]);
+                    aty[3] += tvk * (yn[2] + yn[5]);
+                }
+            }
+            // H dx: the diagonal (eta D_R^2 + Sigma + delta_w) and the constraints' curvature
+            T hx[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hx[j] = qd[j] * dx[j];
+            hx[0] += cv[0] * dx[0];
+            hx[2] += cv[1] * dx[2] + cv[2] * dx[3];
+            hx[3] += cv[2] * dx[2] + cv[4] * dx[5];
+            hx[5] += cv[3] * dx[5] + cv[4] * dx[3];
+            if constexpr (MODEL == 1) {
+                if (!last) {
+                    hx[3] += hvd * dx[6];
+                    hx[6] += hvd * dx[3];
+                }
+            }
+            T* x = xrec(k);
+            const int nv = last ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                T r = 0;
+                if (j < nv) {
+                    const T dr = dR(k, j);
+                    const T rdl = (T)1 / (w[j] - vlo(j)), rdu = (T)1 / (vhi(j) - w[j]);
+                    const T gq = eta * dr * dr * (w[j] - xR(k, j)) - mu * rdl + mu * rdu;
+                    const T jt = j < 6 ? yp[j] - at[j] : (j == 6 ? -twk * (ypn[2] + ypn[5]) : -dt * ypn[3]);
+                    const T jy = j < 6 ? y[j] - aty[j] : (j == 6 ? -twk * (yn[2] + yn[5]) : -dt * yn[3]);
+                    r = -(gq + hx[j] + jt);
+                    rn = tmax(rn, (T)fabs(r));
+                    sn = tmax(sn, (T)fabs(dx[j]));
+                    bn = tmax(bn, (T)fabs(gq + jy));
+                }
+                x[WideLayout::XRX + j] = r;
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const T rsc = rowscale(j, k), irs = rcp(rsc);
+                const T ys = y[j] * irs, ysp = yp[j] * irs;
+                const T p = x[WideLayout::XP + j], n = x[WideLayout::XN + j];
+                const T sp_ = x[WideLayout::XZP + j] / p + dlt, sn_ = x[WideLayout::XZN + j] / n + dlt;
+                const T gpp = (T)RHO - mu / p + (T)KD * mu, gpn = (T)RHO - mu / n + (T)KD * mu;
+                const T dp = x[WideLayout::XDP + j], dn = x[WideLayout::XDN + j], cr = x[WideLayout::XCR + j];
+                const T rp = -(gpp - ysp) - sp_ * dp;
+                const T rq = -(gpn + ysp) - sn_ * dn;
+                const T rc = -cr - (rsc * (dx[j] - (k == 0 ? (T)0 : linp[b][j])) - dp + dn);
+                x[WideLayout::XRP + j] = rp;
+                x[WideLayout::XRN + j] = rq;
+                x[WideLayout::XRC + j] = rc;
+                rn = tmax(rn, tmax(tmax((T)fabs(rp), (T)fabs(rq)), (T)fabs(rc)));
+                sn = tmax(sn, tmax(tmax((T)fabs(dp), (T)fabs(dn)), (T)fabs(ysp - ys)));
+                bn = tmax(bn, tmax(tmax((T)fabs(gpp - ys), (T)fabs(gpn + ys)), (T)fabs(cr)));
+            }
+        }
+        T v[3] = {rn, sn, bn};
+        const int op[3] = {RMAX, RMAX, RMAX};
+        reduce<3, true>(v, op);
+        return wv.uni_d(v[0] / (tmin(v[1], (T)1e6 * v[2]) + v[2]));
+    }
+    // save (to = true) the step in DW, XDP, XDN, YP and the rows' XCR to the records, setting
+    // XCR = -r_c for a correction solve; or add the saved step to the correction there and
+    // restore XCR
+    MPCG_HD void refine_xfer(bool to) {
+        const int t = wv.lane();
+        wv.sync();
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            T* x = xrec(k);
+            const int nv = k == N - 1 ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nv) {
+                    if (to)
+                        x[WideLayout::XSX + j] = ld(L.DW(k) + j);
+                    else
+                        st(L.DW(k) + j, x[WideLayout::XSX + j] + ld(L.DW(k) + j));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                if (to) {
+                    x[WideLayout::XSP + j] = x[WideLayout::XDP + j];
+                    x[WideLayout::XSN + j] = x[WideLayout::XDN + j];
+                    x[WideLayout::XSY + j] = ld(L.YP(k) + j);
+                    x[WideLayout::XSC + j] = x[WideLayout::XCR + j];
+                    x[WideLayout::XCR + j] = -x[WideLayout::XRC + j];
+                } else {
+                    x[WideLayout::XDP + j] = x[WideLayout::XSP + j] + x[WideLayout::XDP + j];
+                    x[WideLayout::XDN + j] = x[WideLayout::XSN + j] + x[WideLayout::XDN + j];
+                    st(L.YP(k) + j, x[WideLayout::XSY + j] + ld(L.YP(k) + j));
+                    x[WideLayout::XCR + j] = x[WideLayout::XSC + j];
+                }
+            }
+        }
+        wv.sync();
+    }
+    // the step before the last correction (the records' XSX, XSP, XSN, XSY)
+    MPCG_HD void refine_undo() {
+        const int t = wv.lane();
+        wv.sync();
+        for (int b = 0; b < NB; ++b) {
+            const int k = t + 64 * b;
+            if (k >= N) continue;
+            T* x = xrec(k);
+            const int nv = k == N - 1 ? 6 : 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < nv) st(L.DW(k) + j, x[WideLayout::XSX + j]);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                x[WideLayout::XDP + j] = x[WideLayout::XSP + j];
+                x[WideLayout::XDN + j] = x[WideLayout::XSN + j];
+                st(L.YP(k) + j, x[WideLayout::XSY + j]);
+            }
+        }
+        wv.sync();
+    }
+    // Ipopt's iterative refinement of the restoration problem's step (PDFullSpaceSolver::Solve
+    // with min_refinement_steps 1, max_refinement_steps 10, residual_ratio_max 1e-10,
+    // residual_improvement_factor 1): the reduced solve (p, n eliminated, AugRestoSystemSolver)
+    // loses digits where a row is nearly hard (Sigma_p, Sigma_n ~ 1e12 near a feasible row at
+    // small mu), and the restoration problem's dual infeasibility then stalls; correction solves
+    // of the same reduced system with the full system's residual as the right-hand side
+    // recover them.  Returns the step statistics of the refined step.
+    MPCG_HD Fwd refine_resto() {
+        T ratio = resid_resto(), old = ratio;
+        for (int it = 1; it <= 10; ++it) {
+            refine_xfer(true);
+            rf_pass = true;
+            const bool ok = wv.uni(riccati(0, sv_delta));
+            if (ok) forward_resto();
+            rf_pass = false;
+            refine_xfer(false);
+            if (!ok) break;  // (the same matrix: cannot fail where the first solve did not)
+            ratio = resid_resto();
+#ifdef MPCG_TRACE
+            if (wv.lane() == 0) printf("  refine %d ratio %.3e (first %.3e)\n", it, (double)ratio, (double)old);
+#endif
+            if (!(ratio > (T)1e-10)) break;
+            if (it > 1 && ratio > old) {  // (no improvement: back to the step before this correction)
+                refine_undo();
+                break;
+            }
+            old = ratio;
+        }
+        return step_stats_resto();
+    }
+
     // fraction to the boundary, grad phi^T d and the relative step of a variable with the
     // lower bound 0 only
     MPCG_HD void dir_one(T v, T z, T gphi, T dv, Fwd& F) const {
@@ -4113,6 +4366,9 @@ struct WideSolver {
             } else if (o == OP_SOLVE) {
                 sv_ok = wv.uni(riccati(sv_mode, sv_delta));
                 if (sv_ok) sv_F = forward(sv_mode);
+                if constexpr (RESTO) {
+                    if (sv_ok) sv_F = refine_resto();
+                }
             } else if (o == OP_TRIAL) {
                 tr_ok = trial(tr_alpha, &tr_phi, &tr_theta);
                 tr_acc = tr_ok && check_acceptability(tr_test, tr_phi, tr_theta);

@@ -90,11 +90,17 @@ class BatchSolver:
         """The solver kernel instance the last solve launched ("k_solve_wide<...>")."""
         return _lib.lib().mpcg_last_kernel(self._h).decode()
 
+    @property
+    def last_solve_order(self) -> bool:
+        """True if the last solve ran its problems expected-longest first (B > 2048)."""
+        return bool(_lib.lib().mpcg_last_solve_order(self._h))
+
     def reserve(self, B: int):
         _lib.check(_lib.lib().mpcg_reserve(self._h, int(B)), "mpcg_reserve")
 
     def workspace_bytes(self, B: int) -> int:
-        return int(_lib.lib().mpcg_workspace_bytes(C.byref(self.params), int(B)))
+        """What reserve(B) allocates (the handle's park capacity and device included)."""
+        return int(_lib.lib().mpcg_handle_workspace_bytes(self._h, int(B)))
 
     # ----------------------------------------------------------------- solve
     def solve(self, state: np.ndarray, coeffs: np.ndarray, want_traj: bool = True) -> dict:

@@ -96,20 +96,23 @@ def test_workspace_bytes(libmpcg):
     flags and counters (slot flags, park count/taken/done, park indices, park ready flags)
     precede them.  N = 20: a slot is 114N + 2*448 = 3176 doubles (rare-path copies and the
     filter entries beyond the 64 held in LDS) rounded to whole 128-byte lines, 3184; a park
-    entry 32 + 2372 (LDS image) + 10524 (a slot, 2372 for the original problem's image, 204N
-    of restoration records and the restoration filter's overflow) = 12928 (whole lines);
+    entry 32 + 2372 (LDS image) + 11684 (a slot, 2372 for the original problem's image, 262N
+    of restoration records -- 190N of them per stage, iterative-refinement residuals and saved
+    steps included -- and the restoration filter's overflow) = 14088, 14096 in whole lines;
     without a GPU the slot count falls back to 4096."""
     from mpc_ros_amd import _lib
 
     p = _lib.MpcgParams()
     libmpcg.mpcg_params_plugin_default(C.byref(p))
     b1 = libmpcg.mpcg_workspace_bytes(C.byref(p), 1)
-    assert b1 == 4 * 256 + (8 * 3184 + 12928) * 8
+    assert b1 == 4 * 256 + (8 * 3184 + 14096) * 8
     b2 = libmpcg.mpcg_workspace_bytes(C.byref(p), 2)
-    assert b2 == 4 * 256 + (16 * 3184 + 2 * 12928) * 8
+    assert b2 == 4 * 256 + (16 * 3184 + 2 * 14096) * 8
     big = libmpcg.mpcg_workspace_bytes(C.byref(p), 65536)
     assert big < 65536 * 3184 * 8 // 4  # (bounded by residency, not by B)
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
+    assert libmpcg.mpcg_handle_workspace_bytes(None, 1) == 0  # (no handle: nothing)
+    assert libmpcg.mpcg_last_solve_order(None) == 0
 
 
 def test_create_without_gpu_fails_loudly(libmpcg):

@@ -57,16 +57,22 @@ def run_harness(exe, P, state, coeffs, opts=None):
                 n_fover=rows[:, 6 + 3 * N].astype(int), nf_peak=rows[:, 7 + 3 * N].astype(int))
 
 
-def compare(r, g, atol=1e-9):
+def compare(r, g, atol=1e-9, iters_exact=1.0):
     """Same status and iteration count, values to rounding -- every row, including those
     on which the oracle runs Ipopt's feasibility-restoration phase (diag[:, 3] > 0), the same
-    number of restoration phases, and no filter entry dropped (Ipopt's filter is unbounded)."""
+    number of restoration phases, and no filter entry dropped (Ipopt's filter is unbounded).
+    iters_exact < 1: the iteration count on at least that fraction of the rows, the others
+    within 2 (SMALL_BOUND_ITERS_EXACT)."""
     if "diag" in g and "n_resto" in r:
         np.testing.assert_array_equal(r["n_resto"], g["diag"][:, 3])
     if "n_fover" in r:
         assert (r["n_fover"] == 0).all()
     np.testing.assert_array_equal(r["status"], g["status"])
-    np.testing.assert_array_equal(r["iters"], g["iters"])
+    if iters_exact >= 1.0:
+        np.testing.assert_array_equal(r["iters"], g["iters"])
+    else:
+        assert np.mean(r["iters"] == g["iters"]) >= iters_exact, (r["iters"], g["iters"])
+        assert np.abs(r["iters"] - g["iters"]).max() <= 2, (r["iters"], g["iters"])
     np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=atol)
     np.testing.assert_allclose(r["traj"], g["traj"], rtol=0, atol=atol)
     fin = np.isfinite(g["obj"])  # (the objective at a non-finite input is not compared)
@@ -150,23 +156,17 @@ def test_wide_core_cpu_time_budget(wide_harness, features_golden, oracle):
     assert (r["status"] == 14).any()
 
 
-def compare_infeasible(r, g, atol=1e-9, min_exact=0.5):
-    """BOUND = 0.4 (small_bound): the NLP is locally infeasible from most starts, and Ipopt
-    ends in its restoration phase -- 5 to 13 phases and up to 78 iterations per problem,
-    with the restoration problem's Newton systems at condition numbers ~1e13.  The device's
-    reduced restoration system (p, n eliminated, Riccati with soft rows) and the oracle's
-    dense Bunch-Kaufman factorisation agree to ~1e-9 per system there; over many phases
-    a line-search decision can flip.  Asserted: the returned controls and trajectory on
-    every row (the last iterate of the original problem), the status on every row the
-    oracle solves, an infeasibility status (5 local infeasibility, or 9 restoration failure)
-    where the oracle reports local infeasibility, and exact status and iteration count on at
-    least min_exact of the rows."""
-    np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=atol)
-    np.testing.assert_allclose(r["traj"], g["traj"], rtol=0, atol=atol)
-    ok = g["status"] != 5
-    np.testing.assert_array_equal(r["status"][ok], g["status"][ok])
-    assert np.isin(r["status"][~ok], (5, 9)).all()
-    assert np.mean((r["status"] == g["status"]) & (r["iters"] == g["iters"])) >= min_exact
+# BOUND = 0.4 (small_bound): the NLP is locally infeasible from most starts, and Ipopt ends in
+# its restoration phase with LOCAL_INFEASIBILITY -- 5 to 13 phases and up to 78 iterations per
+# problem, the restoration problem's Newton systems at condition numbers up to ~1e20 (rows made
+# hard by p, n ~ 1e-12 at mu ~ 1e-9).  The device solves them reduced (p, n eliminated) and
+# refines each step against the full system (Ipopt's iterative refinement, wide_core.h
+# refine_resto); the oracle factors the full system densely.  Compared like every other set --
+# status, restoration count, the returned controls and trajectory on every row -- except that
+# one row of the 16 may take up to two more iterations to meet the restoration problem's
+# tolerance (problem 0: 70 against 69; at mu ~ 1e-9 one reduced step stalls at a residual ratio
+# of 3e-5 where the dense factorisation's is 1e-30).
+SMALL_BOUND_ITERS_EXACT = 15 / 16
 
 
 @pytest.mark.parametrize("name", ["class_defaults", "rate_w", "no_rate", "N40", "N3", "small_bound", "N80", "N100"])
@@ -175,10 +175,7 @@ def test_wide_core_matches_oracle_variants(wide_harness, variants_golden, name):
     n = len(g["status"]) if FULL else (6 if name in ("N3", "small_bound", "class_defaults") else 3)
     sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "traj", "obj", "status", "iters", "diag")}
     r = run_harness(wide_harness, params_from_array(g["params"]), sub["state"], sub["coeffs"])
-    if name == "small_bound":
-        compare_infeasible(r, sub, atol=1e-9)
-    else:
-        compare(r, sub, atol=1e-9)
+    compare(r, sub, atol=1e-9, iters_exact=SMALL_BOUND_ITERS_EXACT if name == "small_bound" else 1.0)
 
 
 def test_wide_core_bicycle_matches_oracle(wide_harness, bicycle_golden):

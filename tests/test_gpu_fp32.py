@@ -103,3 +103,62 @@ def test_fp32_refuses_bicycle(torch_cuda):
 
     with pytest.raises(MpcgError):
         BatchSolver(0, dict(params.PLUGIN_DEFAULTS, STEPS=25, MODEL=1, LF=0.5), dtype="fp32")
+
+
+def test_fp32_escalation_drain_small_batches_park_and_graph(torch_cuda):
+    """The fp32 solver's escalations are always taken: at B = 1 (the park area is one entry, so
+    no concurrent worker holds it and the drain after the batch kernel takes it), with a park
+    area of one entry, and inside a captured HIP graph replayed (a graph executor may run the
+    forked workers before the batch kernel; they exit, the drain remains).  Each escalated row
+    equals its row of the full batch bitwise."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity, params
+    from mpc_ros_amd.solver import BatchSolver
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=40)
+    st, cf = infinity.make_problems(np.arange(4096))
+    s = BatchSolver(0, P, dtype="fp32")
+    a = s.solve(st, cf)
+    esc = np.flatnonzero(a["diag"][:, 2] == 3)
+    assert len(esc) >= 4
+    print("escalated", len(esc), flush=True)
+    for i in esc[:3]:
+        print("B = 1, row", i, flush=True)
+        r = s.solve(st[i:i + 1], cf[i:i + 1])
+        assert r["diag"][0, 2] == 3
+        for k in ("u0", "status", "iters"):
+            np.testing.assert_array_equal(r[k][0], a[k][i])
+    print("park capacity 1", flush=True)
+    s.set_park_capacity(1)
+    b = s.solve(st, cf)
+    s.set_park_capacity(0)
+    for k in ("u0", "status", "iters"):
+        np.testing.assert_array_equal(b[k], a[k])
+    # B = 1 captured in a graph and replayed
+    print("graph", flush=True)
+    i = int(esc[0])
+    dev = torch.device("cuda:0")
+    s.reserve(1)
+    tst, tcf = torch.from_numpy(st[i:i + 1].copy()).to(dev), torch.from_numpy(cf[i:i + 1].copy()).to(dev)
+    u0 = torch.empty((1, 2), dtype=torch.float64, device=dev)
+    status = torch.empty(1, dtype=torch.int32, device=dev)
+    diag = torch.empty((1, 4), dtype=torch.int32, device=dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        s.solve_device(tst, tcf, u0, status=status, diag=diag)
+    torch.cuda.synchronize()
+    print("warm-up", flush=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        s.solve_device(tst, tcf, u0, status=status, diag=diag)
+    print("captured", flush=True)
+    for rep in range(2):
+        u0.zero_()
+        status.zero_()
+        diag.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        print("replay", rep, flush=True)
+        np.testing.assert_array_equal(u0.cpu().numpy()[0], a["u0"][i])
+        assert int(status.cpu()[0]) == a["status"][i] and int(diag.cpu()[0, 2]) == 3

@@ -94,12 +94,34 @@ def test_headline_instance_every_fixture_row(torch_cuda, infinity_golden, featur
     check_against(_sub(r, rest), ref)
 
 
+@pytest.mark.parametrize("B", [4096, 2049])
+def test_configs1_dispatch_every_fixture_row(torch_cuda, infinity_golden, features_golden, oracle, B):
+    """BASELINE configs[1] (B = 4,096, N = 20, fp64) exactly as dispatched: the 512-VGPR
+    instance with the expected-longest-first solve order (B > 2,048).  All 302 default-option
+    N = 20 fixture rows inside the batch and every fresh problem of it against the oracle; the
+    same at B = 2,049, the smallest batch that is ordered."""
+    from mpc_ros_amd import params
+
+    P = params.PLUGIN_DEFAULTS
+    st, cf, exp = _fixture_rows(infinity_golden, features_golden)
+    S, C, pos, rest = _padded(st, cf, B, 9, 7_000_000 + B)
+    s = _solver(P)
+    r = s.solve(S, C)
+    assert s.last_kernel == LONE and s.last_solve_order
+    check_against(_sub(r, pos), exp)
+    check_against(_sub(r, rest), oracle_ref(oracle, P, S[rest], C[rest]))
+    # (results do not depend on the order: an unordered solve of the fixture rows alone)
+    alone = s.solve(st, cf)
+    assert not s.last_solve_order
+    np.testing.assert_array_equal(alone["u0"], r["u0"][pos])
+
+
 def test_small_batches_run_the_lone_instance(torch_cuda, infinity_golden):
     """B <= 4,096 runs the 512-VGPR instance (the fixture-sized tests' instance)."""
     g = infinity_golden
     s = _solver(params_from_array(g["params"]))
     s.solve(g["state"][:64], g["coeffs"][:64])
-    assert s.last_kernel == LONE
+    assert s.last_kernel == LONE and not s.last_solve_order
 
 
 def test_bicycle_instance_at_large_batch(torch_cuda, bicycle_golden, features_golden, oracle):

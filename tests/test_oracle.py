@@ -243,10 +243,11 @@ def test_iterative_refinement_changes_no_fixture_row(oracle, infinity_golden, fe
     refinement restated (ora_ipm_opts.refine_steps = 1) the infinity set and every Ipopt-feature
     set (SOC, watchdog, soft restoration, the restoration phase at N = 20 and 40, the bicycle)
     keep every status, iteration count and restoration count, and u0 moves by rounding only
-    (measured: <= 3.2e-15): omitting it changes no parity claim on these problems.  (The
-    locally infeasible small_bound variant, 5-13 restoration phases at condition numbers
-    ~1e13, is the exception: one row of 16 takes 68 iterations instead of 67, u0 within 1e-11
-    -- tests/test_core_host.py compare_infeasible.)"""
+    (measured: <= 3.2e-15): the dense factorisation is accurate without it.  (The locally
+    infeasible small_bound variant, 5-13 restoration phases at condition numbers up to ~1e20, is
+    the exception: one row of 16 takes 68 iterations instead of 67, u0 within 1e-11.)  The
+    device's reduced restoration solve is not that accurate and refines every restoration step
+    (wide_core.h refine_resto; tests/test_core_host.py SMALL_BOUND_ITERS_EXACT)."""
     sets = [("infinity", infinity_golden, 20, slice(0, 96))]
     for name in ("N20", "N40", "bicycle", "resto_N20", "resto_N40"):
         g = features_golden[name]
