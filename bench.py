@@ -384,7 +384,8 @@ def main():
     # (per-rank status and diagnostic counts, summed over ranks)
     codes = list(range(16))
     mine = torch.tensor([int(np.sum(sts == c)) for c in codes] +
-                        [int(np.sum(dg[:, 0] > 0)), int(dg[:, 0].sum()), int(dg[:, 2].sum()), int(np.sum(dg[:, 1] > 0)),
+                        [int(np.sum(dg[:, 0] > 0)), int(dg[:, 0].sum()), int(np.sum(dg[:, 2] == 1)),
+                         int(np.sum(dg[:, 2] == 3)), int(np.sum(dg[:, 2] == 4)), int(np.sum(dg[:, 1] > 0)),
                          int(dg[:, 3].max(initial=0))], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(mine[:-1])
@@ -445,7 +446,10 @@ def main():
                        "success_frac": float(cnt[1] / total),
                        "status_counts": {str(c): int(cnt[c]) for c in codes if cnt[c]},
                        "restoration": {"problems": int(cnt[16]), "phases": int(cnt[17]), "parked": int(cnt[18])},
-                       "filter": {"problems_dropping_entries": int(cnt[19]), "peak_entries": int(cnt[20])},
+                       # (the fp32 configuration's fp64 phase: problems solved again from the start
+                       # where the fp32 solve did not converge, and continued from its iterate)
+                       "fp64_phase": {"from_start": int(cnt[19]), "continued": int(cnt[20])},
+                       "filter": {"problems_dropping_entries": int(cnt[21]), "peak_entries": int(cnt[22])},
                        "sample": "all problems of the last timed step, all ranks"},
             "timing": {"kernel_ms": kern, "gather_ms": gath, "per_rank": per_rank},
         }

@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libmpcg.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("mpcg_wide.hip", "mpcg_wide_inst.hip", "mpcg_track.hip", "mpcg_synth.hip",
                                            "mpcg_api.cpp", "mpcg_multi.cpp", "mpc_planner.cpp")]
 INST = os.path.join(CSRC, "mpcg_wide_inst.hip")
-N_INST = 10  # MPCG_INST groups of mpcg_wide_inst.hip (mpcg_wide_kern.h)
+N_INST = 12  # MPCG_INST groups of mpcg_wide_inst.hip (mpcg_wide_kern.h)
 HEADERS = [os.path.join(CSRC, f) for f in ("ipm_core.h", "wide_core.h", "wave_dev.h", "mpcg_internal.h",
                                            "mpcg_wide_kern.h")] + [
     os.path.join(ROOT, "include", f) for f in ("mpcg.h", "mpc_planner.h")]
@@ -77,10 +77,12 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              "-mllvm", "-disable-promote-alloca-to-lds", "-mllvm", "-disable-machine-licm",
              "-Wno-unused-result", "-Wno-unused-value",
-             f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{source_hash()}"',
-             "-Rpass-analysis=kernel-resource-usage"]
-    # (diagnostic builds only: extra compiler flags, e.g. -DMPCG_DEBUG_GUARD)
-    flags += os.environ.get("MPCG_EXTRA_CFLAGS", "").split()
+             f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", "-Rpass-analysis=kernel-resource-usage"]
+    # (diagnostic builds only: extra compiler flags, e.g. -DMPCG_DEBUG_GUARD; they are part of
+    # the build id, so such a library never passes for the product: the next build replaces it)
+    extra_flags = os.environ.get("MPCG_EXTRA_CFLAGS", "").split()
+    bid = source_hash() + ("+" + "".join(c for c in "_".join(extra_flags) if c.isalnum() or c == "_") if extra_flags else "")
+    flags += [f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{bid}"'] + extra_flags
     tmp = tempfile.mkdtemp(prefix="mpcg_build_")
     try:
         def cc(unit):

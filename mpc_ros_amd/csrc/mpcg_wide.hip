@@ -24,6 +24,18 @@ __global__ void __launch_bounds__(256) k_sched_key(int64_t B, const double* coef
     idx[p] = (int32_t)p;
 }
 
+// the workspace's per-launch state: the slot flags, the 64 counters (park count / taken / done /
+// started, the overflow count / taken), the park ready flags, the overflow list (-1: not yet
+// published)
+__global__ void __launch_bounds__(256) k_reset_ws(int32_t* flags, int64_t nflags, int32_t* cnt, int32_t* pready,
+                                                  int64_t npready, int64_t* ovf, int64_t novf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nflags) flags[i] = 0;
+    if (i < 64) cnt[i] = 0;
+    if (i < npready) pready[i] = 0;
+    if (i < novf) ovf[i] = -1;
+}
+
 size_t wide_sched_bytes(int64_t B) {
     size_t temp = 0;
     hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const float*)nullptr, (float*)nullptr,
@@ -76,11 +88,14 @@ static const void* rk() {
         return resume_kernel_fn<M, S, T, NB>();
 }
 
-// The fp32 solver does not run the restoration phase itself: a float iterate's line search
-// fails at its noise floor, where a float restoration phase rarely succeeds.  A problem that
-// would enter it is solved again from the start by the fp64 solver with the reference's Ipopt
-// options (mpcg_params.no_restoration = 0, the default; 1 stops it with status 9 instead).
-static bool escalates(const IpmParams& P) { return P.precision == 1 && !P.no_resto; }
+// The fp32 configuration (mpcg_params.precision 1) runs in two phases: the fp32 solver on the
+// whole batch (its stated options), then the fp64 solver with the reference's Ipopt options on
+// the whole batch again (k_warm_wide) -- from the fp32 solver's converged iterate (a few fp64
+// iterations to Ipopt's tolerance), or from the start where the fp32 solve did not converge
+// (its line search fails where Ipopt would enter the restoration phase, a tiny step, the
+// iteration limit: a float iterate's noise floor).  mpcg_params.no_restoration = 1 keeps the
+// fp32 solver's own ending instead (status 9 where Ipopt would restore).
+static bool two_phase(const IpmParams& P) { return P.precision == 1 && !P.no_resto; }
 static IpmParams fp64_params(const IpmParams& P) {
     IpmParams q = P;
     q.precision = 0;
@@ -148,9 +163,9 @@ int device_xccs() {
 
 // Workspace slots for a batch of B: four times the wavefronts the device can hold resident at
 // once (occupancy of the instance at its LDS size times the CUs), at most B (at least 32 per
-// XCD), in one equal partition per XCD (device_xccs).  A wavefront takes the slot its XCD
-// released last (claim_slot: a LIFO stack per partition), so the slots in use stay L2-warm;
-// the margin covers uneven dispatch over the XCDs.
+// XCD), in one equal partition per XCD (device_xccs).  A wavefront claims slot blockIdx mod the
+// partition size in its XCD's partition, or the next free one: with the margin, a slow problem
+// still holding a slot rarely makes a later wavefront probe further.
 int64_t wide_slots(const IpmParams& P, int64_t B) {
     if (B <= 0) return 0;
     int64_t n = 4096;  // (fallback if the runtime cannot say)
@@ -185,25 +200,54 @@ int64_t wide_park_cap(const IpmParams& P, int64_t B) {
     if (P.park_cap > 0) c = P.park_cap;
     return c < B ? c : B;
 }
-// the overflow list: one index per problem (only where the park area can overflow, and for
-// the fp32 solver's escalations)
+// the overflow list: one index per problem (only where the park area can overflow)
 static size_t ovf_bytes(const IpmParams& P, int64_t B) {
-    return wide_park_cap(P, B) < B || escalates(P) ? ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255 : 0;
+    return wide_park_cap(P, B) < B ? ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255 : 0;
 }
 static size_t park_elems(const IpmParams& P);
-// bytes of a park entry (the fp32 solver's escalations: an fp64 problem's)
-static size_t park_entry_bytes(const IpmParams& P) {
-    return escalates(P) ? park_elems(fp64_params(P)) * sizeof(double) : park_elems(P) * elem_bytes(P);
-}
+static size_t park_entry_bytes(const IpmParams& P) { return park_elems(P) * elem_bytes(P); }
 static size_t park_elems(const IpmParams& P) {
     const WideLayout L(P.N, P.filter_cap, P.model);
     const size_t n = (size_t)(32 + L.total() + L.slot()), per_line = 128 / elem_bytes(P);  // (WideSolver::park_elems)
     return (n + per_line - 1) / per_line * per_line;
 }
-size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
+// one phase's workspace: slot flags | counters | park indices | park ready flags | overflow list
+// | slots | park area
+static size_t phase_bytes(const IpmParams& P, int64_t B) {
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     return slot_flag_bytes(ns) + 256 + ((size_t)pc * sizeof(int64_t) + 255 & ~(size_t)255) + slot_flag_bytes(pc) +
            ovf_bytes(P, B) + (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns + park_entry_bytes(P) * (size_t)pc;
+}
+// (the fp32 configuration: the larger phase's workspace -- the phases run one after the other --
+// then the hand-over, WideSolver::handoff_elems floats per problem)
+static size_t handoff_offset(const IpmParams& P, int64_t B) {
+    const size_t a = phase_bytes(P, B), b = phase_bytes(fp64_params(P), B);
+    return ((a > b ? a : b) + 255) & ~(size_t)255;
+}
+static int64_t handoff_stride(const IpmParams& P) {
+    return ((int64_t)(4 + 30 * P.N) + 31) / 32 * 32;  // (WideSolver::handoff_elems, whole lines)
+}
+size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
+    // (+ the fp64 phase's solve order: B indices and two counters)
+    if (two_phase(P))
+        return handoff_offset(P, B) + (size_t)handoff_stride(P) * sizeof(float) * (size_t)B +
+               ((size_t)(B + 63) / 64 * 64 + 64) * sizeof(int32_t);
+    return phase_bytes(P, B);
+}
+
+// The fp64 phase's solve order: the problems the fp32 phase did not converge on (solved from the
+// start: full-length fp64 solves, some through the restoration phase) first, then the others (a
+// few fp64 iterations each), so the long solves do not trail the batch.  Positions by two atomic
+// counters (from the front, and from the back): results do not depend on the order.
+__global__ void __launch_bounds__(256) k_cold_first(int64_t B, const float* h, int64_t stride, const int32_t* order,
+                                                    int32_t* out, int32_t* cnt) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    const int32_t p = order ? order[b] : (int32_t)b;
+    if (h[(int64_t)p * stride] != 0.0f)
+        out[B - 1 - atomicAdd(&cnt[1], 1)] = p;
+    else
+        out[atomicAdd(&cnt[0], 1)] = p;
 }
 
 // Concurrent resume workers (parked problems in flight while the batch kernel runs): each
@@ -222,31 +266,17 @@ static int64_t resume_workers(int64_t B) {
     }();
     return env > 0 ? env : MPCG_RESUME_WORKERS + B / 65536;
 }
-// the fp32 solver's escalations are ~30x more frequent (1.7e-2 of the infinity set at N = 40:
-// 1,127 of 65,536): they are taken while the batch runs by 8 workers and one more per 512
-// problems (136 at 65,536), so few are left for the drain -- each worker holds a SIMD for the
-// batch (13 % of the device at 65,536), but measured at N = 40 the launch takes 35.1 ms with
-// 136 workers, 41.4 ms with 16, 40.0 with 72, 35.4-37.2 with 176-512 (N = 20: 14.95 / 16.15 ms
-// with 136 / 16).  MPCG_ESCALATION_WORKERS overrides the count (a tuning knob, read once).
-static int64_t escalation_workers(int64_t B) {
-    static const int64_t env = [] {
-        const char* s = getenv("MPCG_ESCALATION_WORKERS");
-        return s ? (int64_t)atoll(s) : (int64_t)-1;
-    }();
-    return env > 0 ? env : 8 + B / 512;
-}
-
-hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
-                             double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
-                             const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
-                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join, const char** kernel_name) {
-    if (B <= 0) return hipSuccess;
-    if (!spill) return hipErrorInvalidValue;
+// One batch launch (with its resume workers, drain and overflow launches) of the instance inst
+// for parameters P on the workspace at spill.  handoff: the fp32 configuration's hand-over
+// buffer (the fp32 phase writes it, the fp64 phase -- inst a k_warm_wide instance -- reads it).
+static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t B, const double* state,
+                               const double* coeffs, double* u0, double* traj, int32_t* status, double* obj,
+                               int32_t* iters, int32_t* diag, const int32_t* order, void* spill, float* handoff,
+                               hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join,
+                               int64_t nworkers = -1) {
     const size_t lds = wide_lds_bytes(P);
-    const WideInst inst = wide_kernel(P, B);
     const void* fn = inst.fn;
     if (!fn) return hipErrorInvalidValue;
-    if (kernel_name) *kernel_name = inst.name;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, fn);
@@ -254,12 +284,11 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // the workspace (wide_spill_bytes): slot links | counters: park count, taken, done,
-    // started, overflow count, overflow taken (bytes 0..23), the slot stacks' heads (64..191,
-    // one 8-byte head per XCD) and fresh counters (192..255) | park indices | park ready flags |
-    // overflow list | slots | park area
+    // the workspace (phase_bytes): slot flags | counters: park count, taken, done, started,
+    // overflow count, overflow taken (256 B) | park indices | park ready flags | overflow list |
+    // slots | park area
+    const bool fp32_phase = P.precision == 1 && handoff;  // (parks nothing: its endings go to the hand-over)
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
-    if (ns < 1 || wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
     char* w = (char*)spill;
     int32_t* flags = (int32_t*)w;
     w += slot_flag_bytes(ns);
@@ -274,49 +303,45 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     void* slots = w;
     w += (size_t)slot_elems(P) * elem_bytes(P) * (size_t)ns;
     void* park = w;
-    e = hipMemsetAsync(flags, 0, slot_flag_bytes(ns) + 256, stream);  // (slot links, counters, empty stacks)
-    if (e == hipSuccess) e = hipMemsetAsync(pready, 0, slot_flag_bytes(pc), stream);
-    if (e == hipSuccess && ovf_bytes(P, B)) e = hipMemsetAsync(ovf, 0xFF, ovf_bytes(P, B), stream);  // (all -1)
-    if (e != hipSuccess) return e;
-    const bool esc = escalates(P);
-    // (the fp32 solver's batch parks nothing: every problem that needs the restoration phase
-    // goes to the overflow list)
-    const int nxcc = device_xccs();
-    WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
-               (unsigned long long*)(cnt + 16), cnt + 48,
-               (int32_t)ns, (int32_t)slot_elems(P), cnt, esc ? 0 : (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
-               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)nxcc, 0, 0, 2};
-    void* args[] = {(void*)&a};
-    // the resume workers' arguments: the fp32 solver's escalations run the fp64 solver
-    const IpmParams Pr = esc ? fp64_params(P) : P;
-    WideArgs ar = a;
-    ar.P = Pr;
-    ar.park_stride = (int64_t)park_elems(Pr);
-    if (esc) {
-        ar.phase = 1;
-        ar.ovf_mark = 3;
+    // (the per-launch state -- slot flags, counters, park ready flags, the overflow list at -1 --
+    // reset by a kernel, not by memset nodes: a captured graph replayed a second time ran its
+    // small memsets unordered with the solver kernels)
+    {
+        const int64_t npr = pc, nov = ovf_bytes(P, B) ? B : 0;
+        int64_t n = npr > 64 ? npr : 64;
+        n = n > nov ? n : nov;
+        n = n > ns ? n : ns;
+        hipLaunchKernelGGL(k_reset_ws, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, flags, ns, cnt,
+                           pready, npr, ovf, nov);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    void* rargs[] = {(void*)&ar};
-    const size_t rlds = wide_lds_bytes(Pr);
+    WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
+               (int32_t)ns, (int32_t)slot_elems(P), cnt, fp32_phase ? 0 : (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
+               park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0, 0, 2,
+               handoff, handoff ? handoff_stride(P) : 0};
+    void* args[] = {(void*)&a};
+    if (fp32_phase) {
+        e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
+        return e != hipSuccess ? e : hipGetLastError();
+    }
+    // the resume workers: parked problems (the restoration phase) continued by k_resume_wide
     const void* rf = resume_kernel(P);
+    const size_t rlds = lds;
     e = hipFuncGetAttributes(&fa, rf);
     if (e != hipSuccess) return e;
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
     if (e != hipSuccess) return e;
-    // fork: the resume workers on the aux stream alongside the batch kernel; join: the
-    // stream continues after both (no host synchronisation).  Under graph capture the two
-    // branches need not run concurrently: the workers then exit at once (take_parked) and
-    // the drain takes every parked problem.
-    // (escalations: at most pc - 1 concurrent workers, so the drain after the batch kernel always
-    // has an entry of its own -- the concurrent workers exit after ~2 ms when the batch kernel
-    // has not started, e.g. a graph executor that serialises the fork, and the overflow list
-    // must still be taken.  No worker, no fork: a captured fork whose branch holds no work
-    // deadlocked the second replay of the graph.)
-    const int64_t nw = esc ? escalation_workers(B) : resume_workers(B);
-    const int64_t wmax = esc ? pc - 1 : pc;
+    // fork: the resume workers on the aux stream alongside the batch kernel (the fork point is
+    // before the batch kernel); join: the stream continues after both (no host
+    // synchronisation).  Under graph capture the two branches need not run concurrently: the
+    // workers then exit at once (take_parked) and the drain takes every parked problem.  No
+    // worker, no fork (a captured fork whose branch held no work deadlocked the second replay of
+    // the graph).
+    const int64_t nw = nworkers > 0 ? nworkers : resume_workers(B);
     const bool can_fork = aux && aux != stream && ev_fork && ev_join;
-    const unsigned workers = can_fork ? (unsigned)(wmax < nw ? wmax : nw) : 0u;
+    const unsigned workers = can_fork ? (unsigned)(pc < nw ? pc : nw) : 0u;
     const bool fork = workers > 0;
     if (fork) {
         e = hipEventRecord(ev_fork, stream);
@@ -325,31 +350,24 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     }
     e = hipLaunchKernel(fn, dim3((unsigned)B), dim3(64), args, lds, stream);
     if (e != hipSuccess) return e;
-    if (fork) {  // the concurrent workers (park entries 0 .. workers - 1 for escalations)
-        e = hipLaunchKernel(rf, dim3(workers), dim3(64), rargs, rlds, aux);
+    if (fork) {
+        e = hipLaunchKernel(rf, dim3(workers), dim3(64), args, rlds, aux);
         if (e != hipSuccess) return e;
     }
-    // the drain, after the batch kernel: one worker per park entry (escalations: per park
-    // entry the concurrent workers do not hold), so the problems still waiting when the batch
-    // ends run side by side (a worker finding nothing left exits at once) -- the tail is the
-    // longest restoration, not their sum over a few workers
-    WideArgs ad = ar;
-    ad.ent0 = esc ? (int32_t)workers : 0;
-    void* dargs[] = {(void*)&ad};
-    const unsigned drain = (unsigned)(esc ? pc - workers : pc);
-    if (drain > 0) {
-        e = hipLaunchKernel(rf, dim3(drain), dim3(64), dargs, rlds, stream);
-        if (e != hipSuccess) return e;
-    }
+    // the drain, after the batch kernel: one worker per park entry, so the problems still
+    // waiting when the batch ends run side by side (a worker finding nothing left exits at once)
+    // -- the tail is the longest restoration, not their sum over a few workers
+    e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, rlds, stream);
+    if (e != hipSuccess) return e;
     if (fork) {
         e = hipEventRecord(ev_join, aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
         if (e != hipSuccess) return e;
     }
-    // the park-area overflow (only where it can occur: pc < B), after every worker that
-    // holds a park entry: problems solved again from the start, one per park entry at a time
-    if (!esc && pc < B) {
-        WideArgs ao = ar;
+    // the park-area overflow (only where it can occur: pc < B), after every worker that holds a
+    // park entry: problems solved again from the start, one per park entry at a time
+    if (pc < B) {
+        WideArgs ao = a;
         ao.phase = 1;
         ao.ent0 = 0;
         void* oargs[] = {(void*)&ao};
@@ -357,6 +375,53 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();
+}
+
+// the fp64 phase's instance (k_warm_wide, default options) for the horizon class of P
+static WideInst warm_kernel(const IpmParams& Pr) {
+    const bool split = Pr.N <= 32;
+    const int nb = Pr.N > 64 ? 2 : 1;
+    if (Pr.N > 128 || Pr.model != 0) return WideInst{nullptr, ""};
+    if (nb == 2) return WideInst{warm_kernel_fn<0, false, double, 2, true, 1>(), "k_warm_wide<0,false,double,2,true,1>"};
+    if (split) return WideInst{warm_kernel_fn<0, true, double, 1, true, 2>(), "k_warm_wide<0,true,double,1,true,2>"};
+    if (wide_lds_bytes(Pr) > 32768)
+        return WideInst{warm_kernel_fn<0, false, double, 1, true, 1>(), "k_warm_wide<0,false,double,1,true,1>"};
+    return WideInst{warm_kernel_fn<0, false, double, 1, true, 2>(), "k_warm_wide<0,false,double,1,true,2>"};
+}
+
+hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
+                             double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
+                             const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
+                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join, const char** kernel_name) {
+    if (B <= 0) return hipSuccess;
+    if (!spill) return hipErrorInvalidValue;
+    if (wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
+    const WideInst inst = wide_kernel(P, B);
+    if (!inst.fn) return hipErrorInvalidValue;
+    if (kernel_name) *kernel_name = inst.name;
+    if (!two_phase(P))
+        return launch_phase(P, inst, B, state, coeffs, u0, traj, status, obj, iters, diag, order, spill, nullptr,
+                            stream, aux, ev_fork, ev_join);
+    // the fp32 configuration: the fp32 phase (hand-over, no outputs), then the fp64 phase
+    float* handoff = (float*)((char*)spill + handoff_offset(P, B));
+    hipError_t e = launch_phase(P, inst, B, state, coeffs, u0, traj, status, obj, iters, diag, order, spill, handoff,
+                                stream, aux, ev_fork, ev_join);
+    if (e != hipSuccess) return e;
+    IpmParams Pr = fp64_params(P);
+    const WideInst wi = warm_kernel(Pr);
+    int32_t* order2 = (int32_t*)(handoff + (size_t)handoff_stride(P) * (size_t)B);
+    int32_t* cnt2 = order2 + ((B + 63) / 64) * 64;
+    hipLaunchKernelGGL(k_reset_ws, dim3(1), dim3(256), 0, stream, cnt2, (int64_t)0, cnt2, nullptr, (int64_t)0,
+                       nullptr, (int64_t)0);
+    hipLaunchKernelGGL(k_cold_first, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream, B, (const float*)handoff,
+                       handoff_stride(P), order, order2, cnt2);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // (the problems solved from the start come first and some of them enter the restoration
+    // phase early in the launch: more concurrent resume workers than a batch of the fp64 solver
+    // needs, so they are continued while the rest of the batch runs)
+    return launch_phase(Pr, wi, B, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
+                        aux, ev_fork, ev_join, 8 + B / 2048);
 }
 
 }  // namespace mpcg

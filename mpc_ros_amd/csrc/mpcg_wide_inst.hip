@@ -1,5 +1,5 @@
 // mpc_ros_amd/csrc/mpcg_wide_inst.hip -- the solver kernel instances, one group per
-// translation unit: build.py compiles this file once per MPCG_INST value (0..9, in
+// translation unit: build.py compiles this file once per MPCG_INST value (0..11, in
 // parallel) and links the objects into libmpcg.so.  The groups are listed with their
 // instances in mpcg_wide_kern.h (MPCG_WIDE_SOLVE_INSTANCES / MPCG_WIDE_RESUME_INSTANCES).
 #include "mpcg_wide_kern.h"
@@ -15,6 +15,11 @@ namespace mpcg {
     const void* solve_kernel_fn<M, S, T, NB, D, W>() {                                       \
         return (const void*)k_solve_wide<M, S, T, NB, D, W>;                                  \
     }
+#define MPCG_DEF_WARM(g, M, S, T, NB, D, W)                                                   \
+    template <>                                                                               \
+    const void* warm_kernel_fn<M, S, T, NB, D, W>() {                                        \
+        return (const void*)k_warm_wide<M, S, T, NB, D, W>;                                   \
+    }
 #define MPCG_DEF_RESUME(g, M, S, T, NB)                                                       \
     template <>                                                                               \
     const void* resume_kernel_fn<M, S, T, NB>() {                                            \
@@ -23,6 +28,7 @@ namespace mpcg {
 // (MPCG_SEL_<g>: the instance's definition if g is this unit's group, nothing otherwise)
 #define MPCG_SEL_SOLVE(g, M, S, T, NB, D, W) MPCG_SEL_##g(MPCG_DEF_SOLVE(g, M, S, T, NB, D, W))
 #define MPCG_SEL_RESUME(g, M, S, T, NB) MPCG_SEL_##g(MPCG_DEF_RESUME(g, M, S, T, NB))
+#define MPCG_SEL_WARM(g, M, S, T, NB, D, W) MPCG_SEL_##g(MPCG_DEF_WARM(g, M, S, T, NB, D, W))
 #if MPCG_INST == 0
 #define MPCG_SEL_0(x) x
 #else
@@ -73,7 +79,18 @@ namespace mpcg {
 #else
 #define MPCG_SEL_9(x)
 #endif
+#if MPCG_INST == 10
+#define MPCG_SEL_10(x) x
+#else
+#define MPCG_SEL_10(x)
+#endif
+#if MPCG_INST == 11
+#define MPCG_SEL_11(x) x
+#else
+#define MPCG_SEL_11(x)
+#endif
 MPCG_WIDE_SOLVE_INSTANCES(MPCG_SEL_SOLVE)
 MPCG_WIDE_RESUME_INSTANCES(MPCG_SEL_RESUME)
+MPCG_WIDE_WARM_INSTANCES(MPCG_SEL_WARM)
 
 }  // namespace mpcg

@@ -31,12 +31,7 @@ struct WideArgs {
     int32_t* iters;
     int32_t* diag;         // [B][4] restoration phases, filter overflows, parked (1) / re-solved (2), filter peak (or null)
     void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
-    // the free slots of each XCD's partition: a LIFO stack (claim_slot / release_slot) --
-    // slot_next[s] the slot below s, slot_head[x] (tag << 32 | top + 1) the top of XCD x's
-    // stack, slot_fresh[x] the slots of the partition not yet handed out
-    int32_t* slot_next;
-    unsigned long long* slot_head;
-    int32_t* slot_fresh;
+    int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
     int32_t nslots;        // nxcc partitions of nslots / nxcc slots, one per XCD
     int32_t slot_elems;    // WideLayout::spill() rounded up to whole 128-byte lines
     // parked problems (the restoration phase, continued by k_resume_wide while the batch
@@ -58,11 +53,14 @@ struct WideArgs {
     int64_t* ovf_idx;
     int32_t nxcc;          // XCDs of the device (hipDeviceAttributeNumberOfXccs): slot partitions
     // k_resume_wide: 0 parked problems; 1 the overflow list (solved from the start, in park
-    // entry ent0 + blockIdx.x; diag[:, 2] = ovf_mark: 2 park-area overflow, 3 an fp32 problem
-    // solved again in fp64 where the fp32 solver would enter the restoration phase)
+    // entry ent0 + blockIdx.x; diag[:, 2] = ovf_mark, 2: park-area overflow)
     int32_t phase;
     int32_t ent0;
     int32_t ovf_mark;
+    // the fp32 configuration's hand-over (WideSolver::handoff_out): written by the fp32 batch
+    // kernel, read by k_warm_wide and its resume workers; handoff_stride floats per problem
+    float* handoff;
+    int64_t handoff_stride;
 };
 // the wavefront's end in k_solve_wide (after its results / its parked state are written).
 // No fence: the count only tells the resume workers when every workgroup has finished, and
@@ -81,67 +79,42 @@ __device__ __forceinline__ int xcc_id(int nxcc) {
     return (int)(v & 15) % nxcc;
 }
 
-// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on.  The
-// free slots of a partition form a LIFO stack (Treiber: 64-bit head = ABA tag << 32 | top + 1,
-// the link of each slot in slot_next; slots never handed out are taken from a counter when the
-// stack is empty), so a new problem takes the slot its XCD released last -- its lines are still
-// in that XCD's L2 (dirty ones are overwritten there instead of being written back to HBM:
-// the working set is the resident wavefronts' slots, not the whole partition).  A partition
-// holds 4x the wavefronts an XCD keeps resident, so a claim never waits in practice; with fewer,
-// a wavefront waits for a resident one on its XCD to release its slot.  A slot is only ever
-// touched through one XCD's L2, so handing it over needs no agent-scope fence (an agent release
-// is a write-back of the whole XCD L2, buffer_wbl2, per wavefront: 1.6 GB of write traffic per
-// B = 65,536 launch when it was there).  The hand-over is ordered within the XCD:
-// release_slot waits for the owner's stores to complete (they are in the XCD's L2 then; the
-// vector L1 is write-through) before it links the slot and publishes it (each atomic waited for
-// before the next), and claim_slot invalidates the claiming CU's vector L1 after taking it, so
-// no line a previous owner wrote through another CU is read stale.  Slot lines are whole
-// 128-byte lines, so two XCDs never share one.  Vector atomics, relaxed, on the L2.
-__device__ __forceinline__ int claim_slot(int32_t* next, unsigned long long* head, int32_t* fresh, int nslots,
-                                          int nxcc) {
-    const int x = xcc_id(nxcc), per = nslots / nxcc, base = x * per;
+// A workspace slot for the wavefront's problem, from the partition of the XCD it runs on:
+// the first free one from blockIdx on (a partition holds 4x the wavefronts an XCD keeps
+// resident, so the first probe normally succeeds; with fewer, a wavefront waits for a
+// resident one on its XCD to finish and release its slot).  A slot is therefore only ever
+// touched through one XCD's L2, so handing it over needs no agent-scope fence (an agent
+// release is a write-back of the whole XCD L2, buffer_wbl2, per wavefront: 1.6 GB of write
+// traffic per B = 65,536 launch when it was there).  The hand-over is ordered within the
+// XCD: release_slot waits for the owner's stores to complete (they are in the XCD's L2
+// then; the vector L1 is write-through) before the flag is cleared, and claim_slot
+// invalidates the claiming CU's vector L1 after the flag is taken, so no line a previous
+// owner wrote through another CU is read stale.  Slot lines are whole 128-byte lines, so two
+// XCDs never share one.  Vector atomics (device scope) on the flags.  (Measured in round 5
+// without gain: a per-XCD LIFO free list -- a new problem in the slot its XCD released last --
+// made the headline launch 5x slower, 2,048 wavefronts CAS-ing 8 heads; the slot of the
+// hardware wave slot (HW_REG_HW_ID) kept the time and moved the written bytes per launch
+// both ways: N = 40 763 -> 1,072 MB, bicycle 732 -> 565 MB, fp32 N = 40 1,097 -> 1,176 MB.)
+__device__ __forceinline__ int claim_slot(int32_t* flags, int nslots, int nxcc, int64_t hint) {
+    const int per = nslots / nxcc, base = xcc_id(nxcc) * per;
+    int s = (int)(hint % per);
     int r = 0;
     if (threadIdx.x == 0) {
         for (;;) {
-            const unsigned long long h = __hip_atomic_load(&head[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int top = (int)(h & 0xffffffffull) - 1;
-            if (top >= 0) {
-                const int below = __hip_atomic_load(&next[base + top], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long nh = (((h >> 32) + 1) << 32) | (unsigned long long)(uint32_t)(below + 1);
-                if (atomicCAS(&head[x], h, nh) == h) {
-                    r = base + top;
-                    break;
-                }
-                continue;
-            }
-            const int f = __hip_atomic_load(&fresh[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (f < per) {
-                if (atomicCAS(&fresh[x], f, f + 1) == f) {
-                    r = base + f;
-                    break;
-                }
-                continue;
-            }
-            __builtin_amdgcn_s_sleep(8);
+            if (atomicCAS(&flags[base + s], 0, 1) == 0) break;
+            s = s + 1 == per ? 0 : s + 1;
+            if (s == (int)(hint % per)) __builtin_amdgcn_s_sleep(8);
         }
+        r = base + s;
     }
     r = __builtin_amdgcn_readfirstlane(__shfl(r, 0, 64));
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");  // (acquire: the CU's L1)
     return r;
 }
-__device__ __forceinline__ void release_slot(int32_t* next, unsigned long long* head, int nslots, int nxcc, int s) {
+__device__ __forceinline__ void release_slot(int32_t* flags, int s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (release: the slot's stores are in L2)
     __builtin_amdgcn_wave_barrier();
-    if (threadIdx.x == 0) {
-        const int per = nslots / nxcc, x = s / per;
-        for (;;) {
-            const unsigned long long h = __hip_atomic_load(&head[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicExch(&next[s], (int)(h & 0xffffffffull) - 1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the link is in L2 before the slot is)
-            const unsigned long long nh = (((h >> 32) + 1) << 32) | (unsigned long long)(uint32_t)(s - x * per + 1);
-            if (atomicCAS(&head[x], h, nh) == h) break;
-        }
-    }
+    if (threadIdx.x == 0) atomicExch(&flags[s], 0);
 }
 
 // 2 wavefronts per SIMD: 19 KB of LDS per problem allows 8 problems per CU, the register
@@ -160,8 +133,11 @@ __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t 
 // 3 (168 VGPRs) for the fp32 solver (N <= 64), whose LDS per problem leaves room for more
 // than 8 problems per CU (N = 20: 9.5 KB, 12 per CU; N = 40: 14.8 KB, 11): with 68 VGPRs
 // spilled the split instance is still 13 % faster than at 2 per SIMD
-template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_solve_wide(WideArgs a) {
+// The batch kernels' body: one problem per wavefront.  WARM (the fp64 phase of the fp32
+// configuration, k_warm_wide): the problem continues from the fp32 solver's hand-over
+// (WideSolver::solve_warm) where the fp32 solve converged, else it is solved from the start.
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT, bool WARM>
+__device__ __forceinline__ void solve_body(const WideArgs& a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
     const int t = threadIdx.x;
@@ -175,7 +151,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
     if (blockIdx.x == 0 && t == 0) atomicExch(a.started, 1);
-    int slot = claim_slot(a.slot_next, a.slot_head, a.slot_fresh, a.nslots, a.nxcc);
+    int slot = claim_slot(a.slot_flags, a.nslots, a.nxcc, (int64_t)blockIdx.x);
 #ifdef MPCG_DEBUG_GUARD
     if (t == 0 && (a.B <= 4 || slot < 0 || slot >= a.nslots))
         printf("solve blk %d p %ld slot %d nslots %d xcc %d\n", (int)blockIdx.x, (long)p, slot, a.nslots, xcc_id(a.nxcc));
@@ -183,15 +159,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #endif
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
-    S.solve();
-    // the fp32 solver's problems it cannot finish at a float iterate's noise floor -- the line
-    // search fails where Ipopt would enter its restoration phase (NEED_RESTO) or almost feasible
-    // without an acceptable point (RESTORATION_FAILURE), or it stops at a tiny step or the
-    // iteration limit -- are solved again by the fp64 solver (escalation, unless no_restoration:
-    // the park area is empty for it, so they go to the overflow list)
-    const bool escalate = sizeof(T) == 4 && !Pk.no_resto &&
-                          (S.status == IPM_RESTORATION_FAILURE || S.status == IPM_TINY_STEP || S.status == IPM_MAXITER);
-    if (S.status == Solver::NEED_RESTO || escalate) {
+    if constexpr (WARM) {
+        const float* h = a.handoff + p * a.handoff_stride;
+        if (__builtin_amdgcn_readfirstlane(h[0] != 0.0f ? 1 : 0))
+            S.solve_warm(h);
+        else
+            S.solve();
+    } else {
+        S.solve();
+    }
+    // the fp32 phase of the fp32 configuration: its ending goes to the fp64 phase (k_warm_wide)
+    if constexpr (sizeof(T) == 4) {
+        if (a.handoff) {
+            S.handoff_out(a.handoff + p * a.handoff_stride);
+            release_slot(a.slot_flags, slot);
+            block_done(a.done);
+            return;
+        }
+    }
+    if (S.status == Solver::NEED_RESTO) {
         // the restoration phase runs in k_resume_wide: park the problem
         int e = 0;
         if (t == 0) e = atomicAdd(a.park_count, 1);
@@ -203,7 +189,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __builtin_amdgcn_wave_barrier();
             if (t == 0) atomicExch(&a.park_ready[e], 1);
-            release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
+            release_slot(a.slot_flags, slot);
             block_done(a.done);
             return;
         }
@@ -215,13 +201,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             const int o = atomicAdd(a.ovf_count, 1);
             atomicExch((unsigned long long*)&a.ovf_idx[o], (unsigned long long)p);
         }
-        release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
+        release_slot(a.slot_flags, slot);
         block_done(a.done);
         return;
     }
     write_out(a, S, p, 0);
-    release_slot(a.slot_next, a.slot_head, a.nslots, a.nxcc, slot);
+    release_slot(a.slot_flags, slot);
     block_done(a.done);
+}
+
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_solve_wide(WideArgs a) {
+    solve_body<MODEL, SPLIT, T, NB, DEFOPT, false>(a);
+}
+// the fp64 phase of the fp32 configuration (mpcg_params.precision 1): every problem again, from
+// the fp32 solver's converged iterate (WideSolver::solve_warm) or, where the fp32 solve did not
+// converge, from the start
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT = false, int WPE = 2>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_warm_wide(WideArgs a) {
+    solve_body<MODEL, SPLIT, T, NB, DEFOPT, true>(a);
 }
 
 // results of problem p (u0, status, iterations, objective, trajectory; honor_original_bounds)
@@ -229,10 +227,19 @@ template <class Solver>
 __device__ __forceinline__ void write_out(const WideArgs& a, Solver& S, int64_t p, int parked) {
     const int t = threadIdx.x;
     if (a.diag && t == 0) {
+        // (the fp64 phase of the fp32 configuration: 4 continued from the fp32 iterate, 3 solved
+        // again from the start)
+        if (a.handoff && sizeof(typename Solver::T) == 8) parked = a.handoff[p * a.handoff_stride] != 0.0f ? 4 : 3;
         a.diag[p * 4 + 0] = S.n_resto;
         a.diag[p * 4 + 1] = S.n_fover;
         a.diag[p * 4 + 2] = parked;
         a.diag[p * 4 + 3] = S.nf_peak;
+#ifdef MPCG_DEBUG_MU
+        // (diagnostic build: the barrier parameter at the end of the solve, -100 log10 mu, and
+        // the unscaled complementarity, -100 log10)
+        a.diag[p * 4 + 1] = (int)(-100.0 * log10((double)S.mu));
+        a.diag[p * 4 + 3] = (int)(-100.0 * log10((double)S.compl0 + 1e-300));
+#endif
     }
     const double o = (double)S.objective_out();
     const int N = a.P.N;
@@ -393,6 +400,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
         if (a.phase == 0)
             S.unpark(ent);
+        else if (a.handoff && a.handoff[p * a.handoff_stride] != 0.0f)
+            S.solve_warm(a.handoff + p * a.handoff_stride);  // (the fp32 configuration's fp64 phase)
         else
             S.solve();
         S.finish_resto();
@@ -413,6 +422,8 @@ WideInst wide_kernel(const IpmParams& P, int64_t B);
 int device_xccs();
 template <int MODEL, bool SPLIT, class T, int NB>
 const void* resume_kernel_fn();
+template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT, int WPE>
+const void* warm_kernel_fn();
 
 // (group, model, split, type, blocks, default options, waves per SIMD): the instances the
 // library carries; group = the MPCG_INST translation unit that compiles it
@@ -444,11 +455,20 @@ const void* resume_kernel_fn();
     X(7, 1, true, double, 1)                  \
     X(8, 1, false, double, 1)                 \
     X(9, 1, false, double, 2)
+// the fp64 phase of the fp32 configuration (k_warm_wide), default options: per horizon class
+#define MPCG_WIDE_WARM_INSTANCES(X)           \
+    X(10, 0, true, double, 1, true, 2)        \
+    X(10, 0, false, double, 1, true, 2)       \
+    X(11, 0, false, double, 1, true, 1)       \
+    X(11, 0, false, double, 2, true, 1)
 #define MPCG_DECL_SOLVE(g, M, S, T, NB, D, W) template <> const void* solve_kernel_fn<M, S, T, NB, D, W>();
+#define MPCG_DECL_WARM(g, M, S, T, NB, D, W) template <> const void* warm_kernel_fn<M, S, T, NB, D, W>();
 #define MPCG_DECL_RESUME(g, M, S, T, NB) template <> const void* resume_kernel_fn<M, S, T, NB>();
 MPCG_WIDE_SOLVE_INSTANCES(MPCG_DECL_SOLVE)
 MPCG_WIDE_RESUME_INSTANCES(MPCG_DECL_RESUME)
+MPCG_WIDE_WARM_INSTANCES(MPCG_DECL_WARM)
 #undef MPCG_DECL_SOLVE
+#undef MPCG_DECL_WARM
 #undef MPCG_DECL_RESUME
 
 }  // namespace mpcg

@@ -3554,8 +3554,14 @@ struct WideSolver {
     MPCG_HD void init() {
         setup();
         init_point();
-        mu = wv.uni_d((T)P.mu_init);
-        tau = wv.uni_d(tmax((T)0.99, (T)1 - (T)P.mu_init));
+        reset_state((T)P.mu_init, 0);
+        // least-squares multipliers first (constr_mult_init_max 1000)
+        do_solve(1, (T)0, K_LSQ);
+    }
+    // the solver state at the start of a solve: barrier parameter mu0, iteration count it0
+    MPCG_HD void reset_state(T mu0, int it0) {
+        mu = wv.uni_d(mu0);
+        tau = wv.uni_d(tmax((T)0.99, (T)1 - mu0));
         status = 0;
         theta_max() = -1;
         theta_min = -1;
@@ -3564,7 +3570,7 @@ struct WideSolver {
         acc_alpha = 0;
         acc_z = 0;
         acc_pending = false;
-        iter = 0;
+        iter = it0;
         nf = 0;
         kkt() = 0;
         ref_theta = ref_phi = ref_gd = ref_pgd = ref_pth = 0;
@@ -3585,8 +3591,60 @@ struct WideSolver {
         soc_count = 0;
         lsF = Fwd{(T)1, (T)1, (T)0, (T)0};
         sv_F = lsF;
-        // least-squares multipliers first (constr_mult_init_max 1000)
-        do_solve(1, (T)0, K_LSQ);
+    }
+
+    // The fp32 solver's hand-over to the fp64 solver (BASELINE configs[2], mpcg_params.precision
+    // 1): h[0] 1 if the fp32 solve converged (status 1 or 4: the fp64 solver continues from its
+    // iterate) else 0 (it is solved again from the start), h[1] mu, h[2] iterations, then the
+    // iterate w (8N), z_L (8N), z_U (8N), y (6N) in float (WideLayout's stage-major order).
+    static constexpr int HANDOFF_HEAD = 4;
+    MPCG_HD static int handoff_elems(int N_) { return HANDOFF_HEAD + 30 * N_; }
+    MPCG_HD void handoff_out(float* h) const {
+        const int t_ = wv.lane();
+        wv.sync();
+        if (t_ == 0) {
+            h[0] = (status == IPM_SUCCESS || status == IPM_ACCEPTABLE) ? 1.0f : 0.0f;
+            h[1] = (float)mu;
+            h[2] = (float)iter;
+            h[3] = 0.0f;
+        }
+        float* x = h + HANDOFF_HEAD;
+        for (int e = t_; e < 8 * N; e += 64) {
+            const int k = e >> 3, j = e & 7;
+            x[e] = (float)ld(L.W(k) + j);
+            x[8 * N + e] = (float)ld(L.ZL(k) + j);
+            x[16 * N + e] = (float)ld(L.ZU(k) + j);
+        }
+        for (int e = t_; e < 6 * N; e += 64) {
+            const int k = e / 6, j = e - 6 * k;
+            x[24 * N + e] = (float)ld(L.Y(k) + j);
+        }
+    }
+    // The fp64 solver continued from the fp32 solver's converged iterate (handoff_out): the same
+    // setup (scaling and row scales from the problem's initial state), the iterate, multipliers
+    // and barrier parameter of the fp32 solve, a fresh filter and line-search state, then the
+    // algorithm as from any iterate until Ipopt's fp64 termination test holds.  The iteration
+    // count continues the fp32 solve's.
+    MPCG_HD void solve_warm(const float* h) {
+        setup();
+        init_point();  // (the stage table's constants; the iterate is overwritten)
+        wv.sync();
+        const float* x = h + HANDOFF_HEAD;
+        for (int e = t; e < 8 * N; e += 64) {
+            const int k = e >> 3, j = e & 7;
+            if (k == N - 1 && j >= 6) continue;  // (no control at the last stage)
+            st(L.W(k) + j, (T)x[e]);
+            st(L.ZL(k) + j, (T)x[8 * N + e]);
+            st(L.ZU(k) + j, (T)x[16 * N + e]);
+        }
+        for (int e = t; e < 6 * N; e += 64) {
+            const int k = e / 6, j = e - 6 * k;
+            st(L.Y(k) + j, (T)x[24 * N + e]);
+        }
+        wv.sync();
+        reset_state((T)h[1], (int)h[2]);
+        do_stats(false, (T)0, (T)0, K_BEGIN);
+        run();
     }
 
     // K_LSQ: the least-squares multiplier estimate y0, used if |y0| <= 1000

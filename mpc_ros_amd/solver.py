@@ -16,19 +16,20 @@ from .params import PLUGIN_DEFAULTS
 # Ipopt options of the reference's solve (mpc_planner.cpp:356-368: max_cpu_time 0.5, the
 # rest Ipopt 3.12 defaults); any mpcg_params field can be overridden by keyword
 IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor=1e-8, mu_init=0.1, max_cpu_time=0.5)
-# the fp32 solver (precision 1, BASELINE configs[2]): tolerances a float iterate can meet --
-# the scaled dual infeasibility of an fp32 iterate stalls near 1e-4 (multipliers ~1e3 times
-# FLT_EPSILON) and mu_min = min(tol, compl_inf_tol) / 11 must stay above float resolution
-# Near the solution an fp32 iterate often cannot certify convergence (its dual residual
-# stalls): acceptable termination at 1e-3 and a 300-iteration cap end such stalls (measured
-# on the infinity set: the controls of those problems equal the fp64 solution to ~1e-5).
-# Where the fp32 solver cannot finish -- its line search fails (a float iterate's noise floor)
-# where Ipopt would enter its feasibility-restoration phase, or it is almost feasible without an
-# acceptable point, or it stops at a tiny step or the iteration limit -- the problem is solved
-# again from the start by the fp64 solver with the reference's options (no_restoration = 0;
-# diag[:, 2] == 3 marks it; 1.7 % of the infinity set at N = 40); with no_restoration = 1 it
-# keeps the fp32 ending (status 9, 3 or 2).
-FP32_OPTIONS = dict(precision=1, tol=2e-4, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
+# the fp32 configuration (precision 1, BASELINE configs[2]) runs two phases (mpcg_wide.hip):
+# (1) the fp32 solver on the whole batch with tolerances a float iterate can meet -- the scaled
+#     dual infeasibility of an fp32 iterate stalls near 1e-4 (multipliers ~1e3 times
+#     FLT_EPSILON) and mu_min = min(tol, compl_inf_tol) / 11 must stay above float resolution;
+#     it stops at tol 1e-3 (acceptable termination at 1e-3 and a 300-iteration cap end stalls);
+# (2) the fp64 solver with the reference's Ipopt options on the whole batch again: from the fp32
+#     iterate where the fp32 solve converged (status 1 or 4: a few fp64 iterations to Ipopt's
+#     tolerance, diag[:, 2] == 4), else from the start (its line search failed at a float
+#     iterate's noise floor where Ipopt would enter the restoration phase, a tiny step, the
+#     iteration limit: diag[:, 2] == 3, bitwise the fp64 solver's result).
+# The returned controls are the fp64 solver's (within 1e-6 of the reference's double-precision
+# solve where they converge to the same local minimum).  no_restoration = 1 runs the fp32 phase
+# alone and keeps its ending (status 9, 3 or 2 where it cannot finish).
+FP32_OPTIONS = dict(precision=1, tol=1e-3, compl_inf_tol=1e-2, tiny_step_tol=10 * 1.1920928955078125e-07,
                     acceptable_tol=1e-3, max_iter=300, no_restoration=0)
 
 

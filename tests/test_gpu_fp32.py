@@ -1,17 +1,17 @@
-"""The fp32 solver (BASELINE configs[2]: N = 40, fp32) on the GPU against the fp64 oracle.
+"""The fp32 configuration (BASELINE configs[2]: N = 40, fp32) on the GPU against the fp64 oracle.
 
-Stated tolerance (an fp32 iterate cannot meet Ipopt's tol 1e-8: the solver runs with
-tol 2e-4, compl_inf_tol 1e-2, acceptable_tol 1e-3, tiny_step_tol 10 FLT_EPSILON, max_iter
-300 -- mpc_ros_amd/solver.py FP32_OPTIONS): on the infinity set at N = 40,
-|u0 - u0_fp64| <= 1e-3 on >= 99 % of 4,096 problems (median <= 1e-5), and >= 99.5 % end with
-success or stop_at_acceptable_point (status 1 / 4; measured: all).  The rows beyond 1e-3
-(0.56 % measured) are converged fp32 solves (status 1) that met tol 2e-4 with compl_inf_tol
-1e-2 a few iterations before the fp64 solve met 1e-8: the tolerance, not a failure
-(tools/fp32_diag.py; compl_inf_tol 1e-3 brings them to 0.2 % at 3x the escalations).  Where
-the fp32 solver cannot finish -- its line search fails where Ipopt would enter its
-feasibility-restoration phase, or almost feasible without an acceptable point, or it stops at
-a tiny step or the iteration limit -- the problem is solved again from the start by the fp64
-solver (diag[:, 2] == 3): those rows equal the fp64 solver's bitwise.
+It runs in two phases (mpc_ros_amd/csrc/mpcg_wide.hip): the fp32 solver on the whole batch with
+the stated options a float iterate can meet (solver.py FP32_OPTIONS: tol 1e-3, compl_inf_tol
+1e-2, acceptable_tol 1e-3, tiny_step_tol 10 FLT_EPSILON, max_iter 300), then the fp64 solver
+with the reference's Ipopt options on the whole batch again -- from the fp32 iterate where the
+fp32 solve converged (diag[:, 2] == 4), from the start where it did not (its line search fails
+at a float iterate's noise floor where Ipopt would restore, a tiny step, the iteration limit:
+diag[:, 2] == 3, bitwise the fp64 solver's result).  Stated tolerance, every row:
+|u0 - u0_fp64| <= 1e-3 on all 4,096 N = 40 problems and <= 1e-4 on >= 99.9 % (measured: the
+fp64 phase ends at Ipopt's tol 1e-8, median |du| ~1e-16); every problem ends with status 1 or 4.
+(Round 4's single-phase fp32 solver left 0.56 % of the rows beyond 1e-3, up to 5e-3: float
+rounding at the solution -- those rows ended at the smallest barrier parameter, not at a loose
+one -- which no fp32 tolerance removes.)
 """
 from __future__ import annotations
 
@@ -41,9 +41,11 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
     ref = oracle.mpc_solve_batch(P, st, cf, opts=oracle.ref_opts(40), nthreads=16)
     r = BatchSolver(0, P, dtype="fp32").solve(st, cf)
     assert np.isfinite(r["u0"]).all()
-    assert np.mean(np.isin(r["status"], (1, 4))) >= 0.995 and not np.isin(r["status"], (2, 3, 9, 10)).any()
+    assert np.isin(r["status"], (1, 4)).all()
+    assert np.isin(r["diag"][:, 2], (3, 4)).all()  # (every row through the fp64 phase)
     du = np.abs(r["u0"] - ref["u0"]).max(1)
-    assert np.mean(du <= 1e-3) >= 0.99 and np.median(du) <= 1e-5
+    assert du.max() <= 1e-3, du.max()
+    assert np.mean(du <= 1e-4) >= 0.999 and np.median(du) <= 1e-9
     # controls inside the box
     assert np.abs(r["u0"][:, 0]).max() <= P["ANGVEL"] and np.abs(r["u0"][:, 1]).max() <= P["MAXTHR"]
     # the escalated problems (solved again in fp64): the fp64 solver's results, bitwise
@@ -56,9 +58,10 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
 
 
 def test_fp32_no_restoration_option(torch_cuda):
-    """no_restoration = 1: the fp32 solver keeps its own ending where it would escalate --
-    status 9 where Ipopt would restore, 3 at a tiny step, 2 at the iteration limit; every other
-    row is the same."""
+    """no_restoration = 1: the fp32 phase alone, its own ending kept -- status 9 where Ipopt
+    would restore, 3 at a tiny step, 2 at the iteration limit on exactly the rows the two-phase
+    solve takes from the start in fp64; the other rows converge in fp32 (status 1 or 4) to within
+    the float solver's accuracy of the two-phase result."""
     from mpc_ros_amd import infinity, params
     from mpc_ros_amd.solver import BatchSolver
 
@@ -66,11 +69,10 @@ def test_fp32_no_restoration_option(torch_cuda):
     st, cf = infinity.make_problems(np.arange(4096))
     a = BatchSolver(0, P, dtype="fp32").solve(st, cf)
     b = BatchSolver(0, P, dtype="fp32", no_restoration=1).solve(st, cf)
-    esc = a["diag"][:, 2] == 3
-    assert (b["diag"][:, 2] == 0).all() and np.isin(b["status"][esc], (2, 3, 9)).all()
-    assert not np.isin(b["status"][~esc], (2, 3, 9)).any()
-    np.testing.assert_array_equal(a["status"][~esc], b["status"][~esc])
-    np.testing.assert_array_equal(a["u0"][~esc], b["u0"][~esc])
+    cold = a["diag"][:, 2] == 3
+    assert cold.any() and (b["diag"][:, 2] == 0).all() and np.isin(b["status"][cold], (2, 3, 9)).all()
+    assert np.isin(b["status"][~cold], (1, 4)).all()
+    assert np.abs(a["u0"][~cold] - b["u0"][~cold]).max() <= 1e-2
 
 
 def test_fp32_N40_fixtures(torch_cuda, variants_golden):
@@ -80,7 +82,7 @@ def test_fp32_N40_fixtures(torch_cuda, variants_golden):
     g = variants_golden["N40"]
     r = BatchSolver(0, params_from_array(g["params"]), dtype="fp32").solve(g["state"], g["coeffs"])
     du = np.abs(r["u0"] - g["u0"]).max(1)
-    assert np.mean(du <= 1e-3) >= 0.95
+    assert du.max() <= 1e-3 and np.mean(du <= 1e-6) >= 0.9
 
 
 def test_fp32_N20_and_determinism(torch_cuda, infinity_golden):
@@ -93,7 +95,7 @@ def test_fp32_N20_and_determinism(torch_cuda, infinity_golden):
     b = s.solve(g["state"], g["coeffs"])
     np.testing.assert_array_equal(a["u0"], b["u0"])
     assert np.mean(np.isin(a["status"], (1, 4))) >= 0.97
-    assert np.mean(np.abs(a["u0"] - g["u0"]).max(1) <= 1e-3) >= 0.98  # (incl. the 32 edge cases)
+    assert np.mean(np.abs(a["u0"] - g["u0"]).max(1) <= 1e-3) >= 0.99  # (incl. the 32 edge cases)
 
 
 def test_fp32_refuses_bicycle(torch_cuda):
@@ -105,12 +107,11 @@ def test_fp32_refuses_bicycle(torch_cuda):
         BatchSolver(0, dict(params.PLUGIN_DEFAULTS, STEPS=25, MODEL=1, LF=0.5), dtype="fp32")
 
 
-def test_fp32_escalation_drain_small_batches_park_and_graph(torch_cuda):
-    """The fp32 solver's escalations are always taken: at B = 1 (the park area is one entry, so
-    no concurrent worker holds it and the drain after the batch kernel takes it), with a park
-    area of one entry, and inside a captured HIP graph replayed (a graph executor may run the
-    forked workers before the batch kernel; they exit, the drain remains).  Each escalated row
-    equals its row of the full batch bitwise."""
+def test_fp32_two_phase_small_batches_park_and_graph(torch_cuda):
+    """The two phases at B = 1, with a park area of one entry (the fp64 phase's problems that
+    enter the restoration phase beyond it are solved again -- from the fp32 hand-over where it
+    converged), and inside a captured HIP graph replayed twice (round 4's memset nodes ran
+    unordered on a second replay): each row equals its row of the full batch bitwise."""
     torch = torch_cuda
     from mpc_ros_amd import infinity, params
     from mpc_ros_amd.solver import BatchSolver

@@ -140,9 +140,9 @@ def test_bicycle_instance_at_large_batch(torch_cuda, bicycle_golden, features_go
 
 
 def test_fp32_instance_at_large_batch(torch_cuda, variants_golden):
-    """configs[2]'s instance (fp32, N = 40) at B = 8,192: the N = 40 fixtures inside the batch,
-    within the fp32 tolerance of tests/test_gpu_fp32.py; the rows equal a solo solve of them
-    (results do not depend on batch position)."""
+    """configs[2]'s instance (fp32, N = 40, then the fp64 phase) at B = 8,192: the N = 40 fixtures
+    inside the batch, within the tolerance of tests/test_gpu_fp32.py (every row); the rows equal a
+    solo solve of them (results do not depend on batch position)."""
     g = variants_golden["N40"]
     P = params_from_array(g["params"])
     S, C, pos, _ = _padded(g["state"], g["coeffs"], B_BIG, 6, 4_000_000)
@@ -153,7 +153,7 @@ def test_fp32_instance_at_large_batch(torch_cuda, variants_golden):
     np.testing.assert_array_equal(r["u0"][pos], alone["u0"])
     np.testing.assert_array_equal(r["status"][pos], alone["status"])
     du = np.abs(r["u0"][pos] - g["u0"]).max(1)
-    assert np.mean(du <= 1e-3) >= 0.95
+    assert du.max() <= 1e-3 and np.isin(r["status"], (1, 4)).all()
 
 
 def test_park_area_overflow_matches_oracle(torch_cuda, features_golden, infinity_golden):

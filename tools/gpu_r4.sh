@@ -30,7 +30,7 @@ cfg)
     [ "$c" = lat ] && { timeout -k 10 300 python bench.py --steps 5 --warmup 1 $a > $O/cfg_$c.log 2>&1; rc=$?; }
     echo "$c rc=$rc"; [ $rc -eq 0 ] || exit 1
     tail -1 $O/cfg_$c.log > $O/cfg_$c.json
-    python3 -c "import json; d=json.load(open('$O/cfg_$c.json')); print('  ', round(d['value']), round(d['roofline']['kernel_ms'],3), d['roofline']['kernel'], d['solver']['iters_mean'], d['solver']['status_counts'], d['solver']['restoration'], d.get('latency_b1'))"
+    python3 -c "import json; d=json.load(open('$O/cfg_$c.json')); print('  ', round(d['value']), round(d['roofline']['kernel_ms'],3), d['roofline']['kernel'], d['solver']['iters_mean'], d['solver']['status_counts'], d['solver']['restoration'], d['solver'].get('fp64_phase'), d.get('latency_b1'))"
   done ;;
 stats)
   cd /tmp && export TMPDIR=/tmp

@@ -31,5 +31,11 @@ int main() {
     auto pr = [](const char* n, const std::set<unsigned>& s) { std::printf("%s:", n); for (unsigned x : s) std::printf(" %u", x); std::printf("\n"); };
     pr("se", se); pr("sh", sh); pr("cu", cu); pr("simd", simd); pr("wave", wave); pr("xcc", xcc);
     std::printf("distinct (xcc, se, sh, cu, simd): %zu\n", key.size());
+    std::set<unsigned> full;
+    for (int b = 0; b < B; ++b) {
+        unsigned v = h[2 * b];
+        full.insert(((h[2 * b + 1] & 15) << 20) | (((v >> 13) & 7) << 11) | (((v >> 12) & 1) << 10) | (((v >> 8) & 15) << 6) | (((v >> 4) & 3) << 4) | (v & 15));
+    }
+    std::printf("distinct (xcc, se, sh, cu, simd, wave): %zu\n", full.size());
     return 0;
 }
