@@ -25,7 +25,7 @@ the useful flops of SURVEY.md §8d's formula (iterations x Riccati and forward-p
 per stage, per solve) x the solves of one launch / the launch's average duration
 (HIP events on the stream it runs on), against the FP64 vector peak.  traffic =
 memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3 PMC
-summary of this exact configuration (profiles/r4/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json),
+summary of this exact configuration (profiles/r5/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json),
 or null.  The line also carries hbm = algorithmic bytes per launch (B x 8 x (6 + 4 + 2 +
 3N) = B x 576 B at N = 20) / kernel time against 8 TB/s, and valu_fp64 = PMC-counted
 FP64 lane-FLOPs (redundant lanes included) / kernel time.
@@ -187,7 +187,7 @@ def latency_b1(P, st, cf, solver, dev, reps=50):
 
 def pmc_name(a) -> str:
     """The PMC summary of exactly this configuration (model, mode, dtype, batch, horizon)."""
-    return a.profile_name or f"r4/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}"
+    return a.profile_name or f"r5/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}"
 
 
 def pmc_profile(name):

@@ -109,18 +109,20 @@ typedef struct mpcg_params {
      * (BASELINE configs[2]; differential drive only): iterate, multipliers and Newton systems
      * in float -- state a tolerance a float iterate can meet (tol ~1e-5 instead of 1e-8;
      * tiny_step_tol 10 FLT_EPSILON).  Inputs and outputs stay double.
-     * Escalation (precision 1, no_restoration 0): a problem the fp32 solver cannot finish --
-     * its line search fails where Ipopt would enter the restoration phase, it would end with
-     * 9 (restoration failure), 3 (tiny step) or 2 (max_iter) -- is solved again from the
-     * start by the fp64 solver with the reference's Ipopt options (the 3.12 defaults of the
-     * fields above; only max_cpu_time and the problem parameters are kept from these params).
-     * Such a row reports the fp64 solve: its status, and iters counting only the fp64
-     * iterations; diag[:, 2] = 3 marks it. */
+     * Two phases (precision 1, no_restoration 0): the fp32 solver on the whole batch with these
+     * params' options, then the fp64 solver with the reference's Ipopt options (the 3.12
+     * defaults of the fields above; max_cpu_time and the problem parameters are kept) on the
+     * whole batch again -- from the fp32 iterate, multipliers and barrier parameter where the
+     * fp32 solve converged (status 1 or 4; diag[:, 2] = 4), from the start where it did not (its
+     * line search failed where Ipopt would enter the restoration phase, a tiny step, the
+     * iteration limit; diag[:, 2] = 3, bitwise the fp64 solver's result).  The outputs are the
+     * fp64 phase's; iters counts both phases' iterations for a continued row, the fp64 solve's
+     * for a row solved from the start. */
     int32_t precision;
     /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails (fp32:
-     * the escalation above); 1: stop there with RESTORATION_FAILURE (9) instead, and no fp32
-     * escalation (the fp32 ending is kept).  Occupies the struct's padding: sizeof(mpcg_params)
-     * is unchanged. */
+     * the two phases above); 1: stop there with RESTORATION_FAILURE (9) instead, and for
+     * precision 1 the fp32 phase alone (its ending kept).  Occupies the struct's padding:
+     * sizeof(mpcg_params) is unchanged. */
     int32_t no_restoration;
 } mpcg_params;
 
@@ -194,8 +196,9 @@ int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const do
  * may be NULL): restoration phases entered, filter entries dropped beyond its capacity
  * (filter_cap in LDS plus 448 in the workspace; Ipopt's filter is unbounded, so any nonzero
  * value marks a solve that may differ from Ipopt's), 1 if the problem was continued by the
- * parked-problem kernel (2 if it was solved again after a park-area overflow, 3 if an fp32
- * problem was solved again in fp64 -- the escalation under `precision` -- 0 otherwise), the
+ * parked-problem kernel (2 if it was solved again after a park-area overflow; precision 1: 4 if
+ * the fp64 phase continued from the fp32 iterate, 3 if it solved the problem from the start;
+ * 0 otherwise), the
  * most filter entries held at once (the original problem). */
 int mpcg_solve_ex(mpcg_handle* h, int64_t B, const double* state, const double* coeffs, double* u0, double* traj,
                   int32_t* status, double* obj, int32_t* iters, int32_t* diag);

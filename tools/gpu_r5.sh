@@ -21,9 +21,16 @@ bench)
 cfg)
   TAG=$T STEPS=cfg bash tools/gpu_r4.sh || exit 1 ;;
 pmc)
-  for c in ${PCFGS:-n20:"" n40:"--horizon 40" bic25:"--model bicycle --horizon 25" n40f32:"--horizon 40 --dtype fp32"}; do
-    n=${c%%:*}; a=${c#*:}
-    PTAG=$T PSUF=_$n PASSES="${PPASSES:-fetch write sq grbm flops}" STATS=0 BARGS="$a" bash tools/gpu_pmc.sh || exit 1
+  for c in ${PCFGS:-n20 n40 bic25 n40f32 b4096}; do
+    b=65536
+    case $c in n20) a="";; n40) a="--horizon 40";; bic25) a="--model bicycle --horizon 25";;
+      n40f32) a="--horizon 40 --dtype fp32";; b4096) a="--batch 4096"; b=4096;; esac
+    PTAG=$T PSUF=_$c PBATCH=$b PASSES="${PPASSES:-fetch write sq grbm flops}" STATS=0 BARGS="$a" bash tools/gpu_pmc.sh || exit 1
   done ;;
+stats)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -- python3 $R/bench.py --steps 20 --warmup 2 --cpu-seconds 0 > $O/prof.log 2>&1
+  rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit 1
+  f=$(find $O/prof -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats.csv; cut -c1-150 $O/kernel_stats.csv | head -4; cd $R ;;
 esac
 done
