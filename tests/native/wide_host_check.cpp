@@ -244,6 +244,7 @@ int main() {
     if (std::scanf("%lf %lf %lf", &P.dual_inf_tol, &P.constr_viol_tol, &P.compl_inf_tol) != 3) return 1;
     long B;
     if (std::scanf("%ld", &B) != 1) return 1;
+    const bool two_phase = std::getenv("MPCG_HOST_TWO_PHASE") && std::atoi(std::getenv("MPCG_HOST_TWO_PHASE")) != 0;
     const mpcg::WideLayout L(P.N, P.filter_cap, P.model);
     std::vector<mpcg::IpmProblem<HT>> probs(B);
     for (long b = 0; b < B; ++b) {
@@ -261,13 +262,48 @@ int main() {
         int status = 0, iters = 0, nresto = 0, nfover = 0, nfpeak = 0;
         double obj = 0, u0 = 0, u1 = 0;
         std::vector<double> traj(3 * P.N);
+        // MPCG_HOST_TWO_PHASE=1 (double harness, differential drive, N <= 64): the fp32
+        // configuration's two phases (mpcg_wide.hip) -- the fp32 solver with the given options,
+        // its hand-over, then the fp64 solver with the reference's options from the fp32 iterate
+        // (converged) or from the start (k_warm_wide)
+        const bool two = two_phase && P.model == 0 && P.N <= 64;
+        mpcg::IpmParams Pd = P;
+        if (two) {
+            Pd.precision = 0;
+            mpcg::ipopt_default_options(Pd);
+        }
+        std::vector<float> ho(4 + 30 * P.N), spillf(two ? L.slot() : 0);
         auto lane = [&](int t) {
             HostWave wv{&sh, t, sh.lds.data()};
+            const float* warm = nullptr;
+            if constexpr (std::is_same_v<HT, double>) {
+                if (two) {
+                    mpcg::IpmParams P32 = P;
+                    P32.precision = 1;
+                    mpcg::IpmProblem<float> pf;
+                    for (int j = 0; j < 6; ++j) pf.init[j] = (float)pr.init[j];
+                    for (int j = 0; j < 4; ++j) pf.c[j] = (float)pr.c[j];
+                    if (P.N <= 32) {
+                        mpcg::WideSolver<HostWave, 0, true, float> S32(P32, pf, wv, spillf.data());
+                        S32.solve();
+                        S32.handoff_out(ho.data());
+                    } else {
+                        mpcg::WideSolver<HostWave, 0, false, float> S32(P32, pf, wv, spillf.data());
+                        S32.solve();
+                        S32.handoff_out(ho.data());
+                    }
+                    wv.sync();
+                    warm = ho.data();
+                }
+            }
             auto run = [&](auto& S0) {
                 typedef std::decay_t<decltype(S0)> Solver;
-                S0.solve();
+                if (warm && warm[0] != 0.0f)
+                    S0.solve_warm(warm);
+                else
+                    S0.solve();
                 // a restoration phase: parked and continued as the device's second kernel does
-                Solver S2(P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
+                Solver S2(two ? Pd : P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
                 const bool parked = S0.status == Solver::NEED_RESTO;
                 if (parked) {
                     S0.park(park.data());
@@ -303,10 +339,10 @@ int main() {
                 mpcg::WideSolver<HostWave, 1, false, HT> S(P, pr, wv, spill.data());
                 run(S);
             } else if (P.N <= 32) {
-                mpcg::WideSolver<HostWave, 0, true, HT> S(P, pr, wv, spill.data());
+                mpcg::WideSolver<HostWave, 0, true, HT> S(two ? Pd : P, pr, wv, spill.data());
                 run(S);
             } else {
-                mpcg::WideSolver<HostWave, 0, false, HT> S(P, pr, wv, spill.data());
+                mpcg::WideSolver<HostWave, 0, false, HT> S(two ? Pd : P, pr, wv, spill.data());
                 run(S);
             }
         };

@@ -39,7 +39,7 @@ def opts_line(o) -> str:
             f"{o.cpu_iter_budget} 64\n{o.dual_inf_tol!r} {o.constr_viol_tol!r} {o.compl_inf_tol!r}")
 
 
-def run_harness(exe, P, state, coeffs, opts=None):
+def run_harness(exe, P, state, coeffs, opts=None, env=None):
     from oracle import pyoracle as O
 
     N = int(P["STEPS"])
@@ -50,7 +50,8 @@ def run_harness(exe, P, state, coeffs, opts=None):
            f"{opts_line(o)}\n{len(state)}\n")
     body = "\n".join(" ".join(repr(float(v)) for v in np.concatenate([state[b], coeffs[b]]))
                      for b in range(len(state)))
-    out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True).stdout
+    out = subprocess.run([exe], input=hdr + body + "\n", capture_output=True, text=True, check=True,
+                         env=dict(os.environ, **(env or {}))).stdout
     rows = np.array([r.split() for r in out.strip().split("\n")], dtype=np.float64)
     return dict(status=rows[:, 0].astype(int), iters=rows[:, 1].astype(int), obj=rows[:, 2], u0=rows[:, 3:5],
                 traj=rows[:, 5:5 + 3 * N].reshape(len(state), 3, N), n_resto=rows[:, 5 + 3 * N].astype(int),
@@ -231,3 +232,30 @@ def test_nonfinite_inputs_stop_with_invalid_number(wide_harness, oracle):
     assert g["status"][5] == 1
     r = run_harness(wide_harness, P, st, cf)
     compare(r, g, atol=1e-9)
+
+
+def fp32_opts(oracle, N):
+    """solver.py FP32_OPTIONS as the harness's option line (the fp32 phase's options)."""
+    o = oracle.ref_opts(N)
+    o.tol, o.compl_inf_tol, o.acceptable_tol = 1e-3, 1e-2, 1e-3
+    o.tiny_step_tol, o.max_iter = 10 * 1.1920928955078125e-07, 300
+    return o
+
+
+@pytest.mark.parametrize("name", ["N40", "infinity"])
+def test_wide_core_two_phase_fp32(wide_harness, variants_golden, infinity_golden, oracle, name):
+    """The fp32 configuration's two phases on the host (MPCG_HOST_TWO_PHASE: the float solver
+    with FP32_OPTIONS, its hand-over, then the fp64 solver with the reference's options from the
+    fp32 iterate where it converged, from the start where it did not) against the fp64 oracle's
+    fixtures: every status 1 or 4, every row within 1e-3 (tests/test_gpu_fp32.py's bound), and
+    almost all to the fp64 solve's own accuracy."""
+    g = variants_golden["N40"] if name == "N40" else infinity_golden
+    P = params_from_array(g["params"])
+    n = len(g["status"]) if FULL else 12
+    sub = {k: g[k][:n] for k in ("state", "coeffs", "u0", "status")}
+    r = run_harness(wide_harness, P, sub["state"], sub["coeffs"], opts=fp32_opts(oracle, int(P["STEPS"])),
+                    env={"MPCG_HOST_TWO_PHASE": "1"})
+    assert np.isin(r["status"], (1, 4)).all()
+    du = np.abs(r["u0"] - sub["u0"]).max(1)
+    assert du.max() <= 1e-3, du.max()
+    assert np.mean(du <= 1e-6) >= 0.9
