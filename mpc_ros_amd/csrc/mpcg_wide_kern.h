@@ -162,9 +162,10 @@ __device__ __forceinline__ void solve_body(const WideArgs& a) {
     if constexpr (WARM) {
         const float* h = a.handoff + p * a.handoff_stride;
         if (__builtin_amdgcn_readfirstlane(h[0] != 0.0f ? 1 : 0))
-            S.solve_warm(h);
+            S.init_warm(h);
         else
-            S.solve();
+            S.init();
+        S.run();  // (one call site of the solver's loop)
     } else {
         S.solve();
     }
@@ -398,12 +399,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         DevWave wv;
         wv.t = t;
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
-        if (a.phase == 0)
+        if (a.phase == 0) {
             S.unpark(ent);
-        else if (a.handoff && a.handoff[p * a.handoff_stride] != 0.0f)
-            S.solve_warm(a.handoff + p * a.handoff_stride);  // (the fp32 configuration's fp64 phase)
-        else
-            S.solve();
+        } else {
+            if (a.handoff && a.handoff[p * a.handoff_stride] != 0.0f)
+                S.init_warm(a.handoff + p * a.handoff_stride);  // (the fp32 configuration's fp64 phase)
+            else
+                S.init();
+            S.run();
+        }
         S.finish_resto();
         write_out(a, S, p, a.phase == 0 ? 1 : a.ovf_mark);
     }

@@ -3626,6 +3626,11 @@ struct WideSolver {
     // algorithm as from any iterate until Ipopt's fp64 termination test holds.  The iteration
     // count continues the fp32 solve's.
     MPCG_HD void solve_warm(const float* h) {
+        init_warm(h);
+        run();
+    }
+    // (the state solve_warm runs from: callers with one run() call site use init_warm / init)
+    MPCG_HD void init_warm(const float* h) {
         setup();
         init_point();  // (the stage table's constants; the iterate is overwritten)
         wv.sync();
@@ -3644,7 +3649,6 @@ struct WideSolver {
         wv.sync();
         reset_state((T)h[1], (int)h[2]);
         do_stats(false, (T)0, (T)0, K_BEGIN);
-        run();
     }
 
     // K_LSQ: the least-squares multiplier estimate y0, used if |y0| <= 1000
