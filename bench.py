@@ -84,8 +84,9 @@ def parse():
                     help="launch/shard/gather plumbing only: gloo on CPU, a stub solver that writes each "
                          "problem's global index (tests/test_bench_launch.py); no GPU, no timing claim")
     ap.add_argument("--restoration", default="auto", choices=["auto", "on", "off"],
-                    help="Ipopt's feasibility-restoration phase: auto = the dtype's default (fp64 on; the fp32 "
-                         "solver's FP32_OPTIONS off), on / off = mpcg_params.no_restoration 0 / 1")
+                    help="Ipopt's feasibility-restoration phase: auto = the dtype's default (fp64: on; fp32: the "
+                         "two phases, fp32 then fp64), on / off = mpcg_params.no_restoration 0 / 1 (fp32 off: the "
+                         "fp32 phase alone)")
     ap.add_argument("--inputs", default="device", choices=["device", "host"],
                     help="where each rank generates its shard of the synthetic robots from (seed, global index): "
                          "device = mpcg_synth_infinity_device + the device preprocessing (findBestPath); host = "
@@ -187,7 +188,8 @@ def latency_b1(P, st, cf, solver, dev, reps=50):
 
 def pmc_name(a) -> str:
     """The PMC summary of exactly this configuration (model, mode, dtype, batch, horizon)."""
-    return a.profile_name or f"r5/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}"
+    off = "_norestoration" if getattr(a, "restoration", "on") == "off" else ""
+    return a.profile_name or f"r5/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}{off}"
 
 
 def pmc_profile(name):
