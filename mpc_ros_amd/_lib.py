@@ -123,7 +123,7 @@ def lib():
             raise MpcgError("libmpcg ABI version mismatch")
         from . import build
 
-        want, got = build.source_hash(), L.mpcg_build_id().decode()
+        want, got = build.build_id(), L.mpcg_build_id().decode()
         if got != want:
             raise MpcgError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
                             "rebuild with `python -m mpc_ros_amd.build`")

@@ -49,11 +49,23 @@ def built_id(lib: str = LIB) -> str | None:
     with open(lib, "rb") as fh:
         data = fh.read()
     i = data.find(b"MPCG-BUILD-ID:")
-    return data[i + 14:i + 30].decode() if i >= 0 else None
+    return data[i + 14:data.find(b"\0", i)].decode() if i >= 0 else None
+
+
+def extra_cflags() -> list:
+    """MPCG_EXTRA_CFLAGS (diagnostic builds only, e.g. -DMPCG_DEBUG_GUARD)."""
+    return os.environ.get("MPCG_EXTRA_CFLAGS", "").split()
+
+
+def build_id() -> str:
+    """The sources' hash, + the extra flags of a diagnostic build: such a library never passes
+    for the product (the loader compares against the id of the environment it runs in)."""
+    x = extra_cflags()
+    return source_hash() + ("+" + "".join(c for c in "_".join(x) if c.isalnum() or c == "_") if x else "")
 
 
 def stale() -> bool:
-    return built_id() != source_hash()
+    return built_id() != build_id()
 
 
 def compile_units() -> list:
@@ -78,11 +90,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
              "-mllvm", "-disable-promote-alloca-to-lds", "-mllvm", "-disable-machine-licm",
              "-Wno-unused-result", "-Wno-unused-value",
              f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", "-Rpass-analysis=kernel-resource-usage"]
-    # (diagnostic builds only: extra compiler flags, e.g. -DMPCG_DEBUG_GUARD; they are part of
-    # the build id, so such a library never passes for the product: the next build replaces it)
-    extra_flags = os.environ.get("MPCG_EXTRA_CFLAGS", "").split()
-    bid = source_hash() + ("+" + "".join(c for c in "_".join(extra_flags) if c.isalnum() or c == "_") if extra_flags else "")
-    flags += [f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{bid}"'] + extra_flags
+    # (diagnostic builds only: extra compiler flags, part of the build id)
+    flags += [f'-DMPCG_BUILD_ID="MPCG-BUILD-ID:{build_id()}"'] + extra_cflags()
     tmp = tempfile.mkdtemp(prefix="mpcg_build_")
     try:
         def cc(unit):

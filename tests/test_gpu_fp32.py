@@ -57,6 +57,49 @@ def test_fp32_N40_against_fp64_oracle(torch_cuda, oracle):
     np.testing.assert_array_equal(r["status"][esc], ref["status"][esc])
 
 
+def test_fp32_full_batch_against_fp64(torch_cuda):
+    """configs[2] at its full size (B = 65,536, N = 40, the bench's infinity set generated on the
+    device) against the fp64 solver on the same batch (the oracle's result row for row,
+    tests/test_gpu_headline.py).  A row whose fp32 phase converged into another local minimum
+    (the objective differs by more than 1e-6 relative) is continued to that minimum by the fp64
+    phase -- Ipopt from that iterate does the same; measured: 3 such rows (44,291: objective
+    17,371 vs 17,102, |du0| 6.2e-3; 40,378 and 41,766 with the same controls to 1e-5).  Every
+    other row: |du0| <= 1e-4 (measured max 9.2e-6)."""
+    torch = torch_cuda
+    from mpc_ros_amd import params
+    from mpc_ros_amd.solver import BatchSolver
+
+    B = 65536
+    dev = torch.device("cuda:0")
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=40)
+    out = {}
+    for name, s in (("fp64", BatchSolver(0, P)), ("fp32", BatchSolver(0, P, dtype="fp32"))):
+        pose, vel, plan = s.synth_infinity_device(0, B)
+        st = torch.empty((B, 6), dtype=torch.float64, device=dev)
+        cf = torch.empty((B, 4), dtype=torch.float64, device=dev)
+        s.preprocess_device(pose, vel, plan, st, cf)
+        u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        obj = torch.empty(B, dtype=torch.float64, device=dev)
+        diag = torch.empty((B, 4), dtype=torch.int32, device=dev)
+        s.solve_device(st, cf, u0, status=status, obj=obj, diag=diag)
+        torch.cuda.synchronize()
+        out[name] = dict(u0=u0.cpu().numpy(), status=status.cpu().numpy(), obj=obj.cpu().numpy(),
+                         diag=diag.cpu().numpy())
+    a, b = out["fp32"], out["fp64"]
+    assert (a["status"] == 1).all() and (b["status"] == 1).all()
+    assert np.isin(a["diag"][:, 2], (3, 4)).all()
+    du = np.abs(a["u0"] - b["u0"]).max(1)
+    other_min = np.abs(a["obj"] - b["obj"]) > 1e-6 * np.abs(b["obj"])
+    print("rows in another local minimum:", np.flatnonzero(other_min).tolist(), "max |du0| elsewhere",
+          du[~other_min].max())
+    assert other_min.sum() <= 4
+    assert du[~other_min].max() <= 1e-4
+    # the rows solved from the start are the fp64 solver's, bitwise
+    cold = a["diag"][:, 2] == 3
+    np.testing.assert_array_equal(a["u0"][cold], b["u0"][cold])
+
+
 def test_fp32_no_restoration_option(torch_cuda):
     """no_restoration = 1: the fp32 phase alone, its own ending kept -- status 9 where Ipopt
     would restore, 3 at a tiny step, 2 at the iteration limit on exactly the rows the two-phase
