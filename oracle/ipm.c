@@ -41,7 +41,8 @@
  *
  * Not restated (documented in DESIGN.md): Ipopt's iterative refinement of the KKT
  * solution (the dense LDL^T solve here is accurate to rounding), slack moves for
- * slacks below eps*mu (AdjustedTrialSlacks; slacks here stay >= ~1e-11), and a
+ * slacks below eps*min(1,mu) (AdjustedTrialSlacks: never triggered on the fixtures -- the
+ * smallest margin is recorded, ora_ipm_result.min_slack_margin), and a
  * restoration phase inside the restoration phase (a failed line search of the
  * restoration problem returns RESTORATION_FAILURE).  The restoration phase is
  * restated for equality-constrained problems (the MPC NLP has no inequality rows).
@@ -271,6 +272,7 @@ struct ipm {
     double *acc_w, *acc_y, *acc_zL, *acc_zU;
     int resto_first;   /* restoration problem: first convergence check */
     ora_ipm_result* diag;
+    ora_ipm_result* slk; /* the slack margins (barrier_phi), the restoration problem's too */
     double* mem;
     /* kkt_structured: position of KKT row i in the banded order, envelope of the factor */
     int *kpos, *klast;
@@ -339,6 +341,12 @@ static double barrier_phi(ipm* S, const double* w, int* ok) {
     iprob* P = S->P;
     const double kd = 1e-5, mu = S->mu;
     double phi = P->f(P, w, mu);
+    /* Ipopt moves a slack below eps * min(1, mu) (CalculateSafeSlack) and then relaxes that
+     * bound (AcceptTrialPoint, AdjustedTrialSlacks): not restated -- the smallest margin
+     * s / (eps min(1, mu)) of every point whose barrier is evaluated is recorded instead,
+     * so a test can show the move never triggers (tests/test_oracle.py) */
+    const double smin = EPS_MACH * fmin(1.0, mu);
+    double rmin = INFINITY;
     *ok = 1;
     for (int i = 0; i < S->nw; ++i) {
         if (P->hasL[i]) {
@@ -346,15 +354,21 @@ static double barrier_phi(ipm* S, const double* w, int* ok) {
             if (!(d > 0)) { *ok = 0; return INFINITY; }
             phi -= mu * log(d);
             if (!P->hasU[i]) phi += kd * mu * d;
+            rmin = fmin(rmin, d / smin);
         }
         if (P->hasU[i]) {
             double d = P->wu[i] - w[i];
             if (!(d > 0)) { *ok = 0; return INFINITY; }
             phi -= mu * log(d);
             if (!P->hasL[i]) phi += kd * mu * d;
+            rmin = fmin(rmin, d / smin);
         }
     }
     if (!isfinite(phi)) *ok = 0;
+    if (S->slk) {
+        if (rmin < S->slk->min_slack_margin) S->slk->min_slack_margin = rmin;
+        if (rmin < 1.0) ++S->slk->n_slack_moves;
+    }
     return phi;
 }
 static void barrier_grad(ipm* S, const double* w, const double* gf, double* gphi) {
@@ -904,6 +918,7 @@ static int perform_restoration(ipm* S) {
     Rs.outer = S;
     Rs.iter = S->iter;
     Rs.diag = NULL;
+    Rs.slk = S->slk;
     Rs.resto_first = 1;
     /* RestoIterateInitializer: mu_R = max(mu, ||c||_inf), p and n the minimisers of the
      * l1 penalty with barrier for fixed x, x bound multipliers min(rho, z), p/n
@@ -1333,7 +1348,9 @@ int ora_ipm_solve(const ora_nlp* nlp, const ora_ipm_opts* opts_in, double* x_out
     S.iter = &iter;
     ora_ipm_result diag;
     memset(&diag, 0, sizeof diag);
+    diag.min_slack_margin = INFINITY;
     S.diag = &diag;
+    S.slk = &diag;
 
     /* ---- starting point: x0 pushed inside (bound_push/bound_frac 0.01) ---- */
     for (int i = 0; i < n; ++i) S.w[i] = nlp->x0[i];

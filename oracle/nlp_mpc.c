@@ -340,12 +340,14 @@ int ora_mpc_solve_batch_diag(const ora_mpc_params* p, const ora_ipm_opts* opts, 
         if (status) status[b] = st;
         if (iters) iters[b] = res.iters;
         if (diag) {
-            int32_t* d = diag + 5 * b;
+            int32_t* d = diag + 7 * b;
             d[0] = res.n_soc;
             d[1] = res.n_watchdog;
             d[2] = res.n_soft_resto;
             d[3] = res.n_resto;
             d[4] = res.resto_iters;
+            d[5] = res.n_slack_moves;
+            d[6] = (int32_t)floor(log10(fmax(fmin(res.min_slack_margin, 1e300), 1e-300)));
         }
     }
     return 0;

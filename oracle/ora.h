@@ -128,6 +128,11 @@ typedef struct ora_ipm_result {
     /* diagnostics: second-order corrections accepted, watchdog activations, soft
      * restoration steps, restoration phases entered, restoration-phase iterations */
     int n_soc, n_watchdog, n_soft_resto, n_resto, resto_iters;
+    /* the smallest slack of any point whose barrier was evaluated (original and restoration
+     * problem) over eps * min(1, mu), and how many points fell below 1: Ipopt would move
+     * those slacks (CalculateSafeSlack / AdjustedTrialSlacks, not restated) */
+    double min_slack_margin;
+    int n_slack_moves;
     /* x[n], zl[n], zu[n], lambda[m], g[m] written to caller buffers */
 } ora_ipm_result;
 

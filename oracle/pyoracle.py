@@ -176,12 +176,13 @@ def mpc_solve_batch(params: dict, state: np.ndarray, coeffs: np.ndarray, opts: I
     obj = np.zeros(B)
     status = np.zeros(B, dtype=np.int32)
     iters = np.zeros(B, dtype=np.int32)
-    dg = np.zeros((B, 5), dtype=np.int32)
+    dg = np.zeros((B, 7), dtype=np.int32)
     L.ora_mpc_solve_batch_diag(C.byref(p), C.byref(o), B, _dp(st), _dp(cf), _dp(u0), _dp(traj), _dp(obj),
                                status.ctypes.data_as(C.POINTER(C.c_int32)), iters.ctypes.data_as(C.POINTER(C.c_int32)),
                                dg.ctypes.data_as(C.POINTER(C.c_int32)), int(nthreads))
     out = dict(u0=u0, traj=traj, obj=obj, status=status, iters=iters)
-    if diag:  # per problem: n_soc, n_watchdog, n_soft_resto, n_resto, resto_iters
+    if diag:  # per problem: n_soc, n_watchdog, n_soft_resto, n_resto, resto_iters, slack moves
+        # (never restated: must be 0), floor(log10(smallest slack / (eps min(1, mu))))
         out["diag"] = dg
     return out
 

@@ -196,7 +196,7 @@ def test_oracle_ipopt_mechanisms_fire_and_reproduce(oracle, features_golden):
         r = oracle.mpc_solve_batch(P, g["state"], g["coeffs"], opts=oracle.ref_opts(int(P["STEPS"])), diag=True)
         np.testing.assert_array_equal(r["status"], g["status"])
         np.testing.assert_array_equal(r["iters"], g["iters"])
-        np.testing.assert_array_equal(r["diag"], g["diag"])
+        np.testing.assert_array_equal(r["diag"][:, :5], g["diag"])  # (the fixtures: the first five)
         np.testing.assert_allclose(r["u0"], g["u0"], rtol=0, atol=1e-12)
         seen |= (g["diag"][:, :4] > 0).any(0)
         for b in np.where(g["diag"][:, 3] > 0)[0][:3]:
@@ -260,3 +260,32 @@ def test_iterative_refinement_changes_no_fixture_row(oracle, infinity_golden, fe
         np.testing.assert_array_equal(r["iters"], g["iters"][sl], err_msg=name)
         np.testing.assert_array_equal(r["diag"][:, 3], g["diag"][sl, 3], err_msg=name)
         np.testing.assert_allclose(r["u0"], g["u0"][sl], rtol=0, atol=1e-13, err_msg=name)
+
+
+def test_unrestated_ipopt_paths_never_reached(oracle, infinity_golden, features_golden, variants_golden):
+    """Two parts of Ipopt 3.12 are not restated (oracle/ipm.c header), and this shows no fixture
+    row reaches them:
+    - the slack move (IpoptCalculatedQuantities::CalculateSafeSlack, then AcceptTrialPoint's
+      AdjustedTrialSlacks bound relaxation) acts on a slack below eps * min(1, mu); the oracle
+      records the smallest slack / (eps min(1, mu)) of every point whose barrier it evaluates,
+      original and restoration problem: no point falls below 1 (measured: >= 1e8 on every set but
+      the locally infeasible small_bound, 1e3 there);
+    - the restoration phase of the restoration problem (RestoRestorationPhase) runs only where the
+      restoration problem's line search fails, which is where the oracle (and the device) return
+      RESTORATION_FAILURE (9): no row ends with 9."""
+    sets = [("infinity", infinity_golden, None)]
+    for name in ("N20", "N40", "bicycle", "resto_N20", "resto_N40"):
+        sets.append((name, features_golden[name], None))
+    for name in ("class_defaults", "no_rate", "rate_w", "N40", "N3", "small_bound", "N80", "N100"):
+        sets.append((name, variants_golden[name], None))
+    worst = []
+    for name, g, _ in sets:
+        P = g["P"] if "P" in g else params_from_array(g["params"])
+        r = oracle.mpc_solve_batch(P, g["state"], g["coeffs"], opts=oracle.ref_opts(int(P["STEPS"])), nthreads=8,
+                                   diag=True)
+        np.testing.assert_array_equal(r["status"], g["status"], err_msg=name)
+        assert (r["diag"][:, 5] == 0).all(), (name, np.flatnonzero(r["diag"][:, 5]))
+        assert (r["status"] != 9).all(), name
+        worst.append((name, int(r["diag"][:, 6].min())))
+    print("floor(log10(smallest slack margin)) per set:", worst)
+    assert min(w for _, w in worst) >= 0
