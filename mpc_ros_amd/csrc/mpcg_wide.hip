@@ -274,7 +274,11 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
                                int32_t* iters, int32_t* diag, const int32_t* order, void* spill, float* handoff,
                                hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join,
                                int64_t nworkers = -1) {
-    const size_t lds = wide_lds_bytes(P);
+    size_t lds = wide_lds_bytes(P);
+#ifdef MPCG_LDS_PAD_ENV
+    // (diagnostic builds only: extra LDS per workgroup, fewer problems per CU)
+    if (const char* pad = getenv("MPCG_LDS_PAD")) lds += (size_t)atol(pad);
+#endif
     const void* fn = inst.fn;
     if (!fn) return hipErrorInvalidValue;
     // the solver addresses its dynamic LDS from address 0 (wave_dev.h): no static LDS
