@@ -288,10 +288,21 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
     if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    const bool fp32_phase = P.precision == 1 && handoff;  // (parks nothing: its endings go to the hand-over)
+    // (every host-side call before the first launch: the device does not wait for the host
+    // between the reset kernel and the solver -- ~15 us of a B = 1 solve otherwise)
+    const void* rf = fp32_phase ? nullptr : resume_kernel(P);
+    const size_t rlds = lds;
+    if (rf) {
+        e = hipFuncGetAttributes(&fa, rf);
+        if (e != hipSuccess) return e;
+        if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+        e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
+        if (e != hipSuccess) return e;
+    }
     // the workspace (phase_bytes): slot flags | counters: park count, taken, done, started,
     // overflow count, overflow taken (256 B) | park indices | park ready flags | overflow list |
     // slots | park area
-    const bool fp32_phase = P.precision == 1 && handoff;  // (parks nothing: its endings go to the hand-over)
     const int64_t ns = wide_slots(P, B), pc = wide_park_cap(P, B);
     char* w = (char*)spill;
     int32_t* flags = (int32_t*)w;
@@ -330,13 +341,6 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
         return e != hipSuccess ? e : hipGetLastError();
     }
     // the resume workers: parked problems (the restoration phase) continued by k_resume_wide
-    const void* rf = resume_kernel(P);
-    const size_t rlds = lds;
-    e = hipFuncGetAttributes(&fa, rf);
-    if (e != hipSuccess) return e;
-    if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
-    e = hipFuncSetAttribute(rf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
-    if (e != hipSuccess) return e;
     // fork: the resume workers on the aux stream alongside the batch kernel (the fork point is
     // before the batch kernel); join: the stream continues after both (no host
     // synchronisation).  Under graph capture the two branches need not run concurrently: the
@@ -344,7 +348,9 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
     // worker, no fork (a captured fork whose branch held no work deadlocked the second replay of
     // the graph).
     const int64_t nw = nworkers > 0 ? nworkers : resume_workers(B);
-    const bool can_fork = aux && aux != stream && ev_fork && ev_join;
+    // (B = 1: a parked problem is the whole batch, the drain continues it as soon as a worker
+    // would -- no fork, no worker spinning beside the solve)
+    const bool can_fork = B > 1 && aux && aux != stream && ev_fork && ev_join;
     const unsigned workers = can_fork ? (unsigned)(pc < nw ? pc : nw) : 0u;
     const bool fork = workers > 0;
     if (fork) {
