@@ -117,7 +117,9 @@ typedef struct mpcg_params {
      * line search failed where Ipopt would enter the restoration phase, a tiny step, the
      * iteration limit; diag[:, 2] = 3, bitwise the fp64 solver's result).  The outputs are the
      * fp64 phase's; iters counts both phases' iterations for a continued row, the fp64 solve's
-     * for a row solved from the start. */
+     * for a row solved from the start.  Batches of more than 2,048 (solved in expected-longest-
+     * first order): the B / 1024 problems ranked longest are solved by the fp64 solver from the
+     * start (diag[:, 2] = 3) while the fp32 phase runs the others. */
     int32_t precision;
     /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails (fp32:
      * the two phases above); 1: stop there with RESTORATION_FAILURE (9) instead, and for

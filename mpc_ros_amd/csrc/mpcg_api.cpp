@@ -38,6 +38,9 @@ struct mpcg_handle {
     // join events on the caller's stream)
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // (the fp32 configuration's head runs on aux, its resume workers on aux2)
+    hipStream_t aux2 = nullptr;
+    hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
     mpcg_params params{};
     // staging buffers for mpcg_solve (host pointers)
     double* d_io = nullptr;
@@ -280,7 +283,7 @@ static mpcg::IpmParams to_ipm(const mpcg_params& p) {
 }
 
 // solve-order buffers (batches beyond the resident wavefronts)
-static const int64_t kOrderMinBatch = 2048;
+using mpcg::kOrderMinBatch;
 static mpcg::IpmParams handle_ipm(const mpcg_handle* h);
 
 size_t mpcg_workspace_bytes(const mpcg_params* p, int64_t B) {
@@ -322,6 +325,9 @@ int mpcg_create(int device, mpcg_handle** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join2, hipEventDisableTiming);
     if (e != hipSuccess) {
         mpcg_destroy(h);
         return hip_fail(e, "hipEventCreate / hipStreamCreate");
@@ -342,10 +348,14 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->d_spill) hipFree(h->d_spill);
     if (h->d_arc) hipFree(h->d_arc);
     if (h->aux) hipStreamSynchronize(h->aux);
+    if (h->aux2) hipStreamSynchronize(h->aux2);
     if (h->last_ev) hipEventDestroy(h->last_ev);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
+    if (h->ev_fork2) hipEventDestroy(h->ev_fork2);
+    if (h->ev_join2) hipEventDestroy(h->ev_join2);
     if (h->aux) hipStreamDestroy(h->aux);
+    if (h->aux2) hipStreamDestroy(h->aux2);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -484,9 +494,15 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
         if (e != hipSuccess) return hip_fail(e, "solve-order sort");
         order = ord;
     }
+    mpcg::WideStreams ws;
+    ws.aux = h->aux;
+    ws.aux2 = h->aux2;
+    ws.ev_fork = h->ev_fork;
+    ws.ev_join = h->ev_join;
+    ws.ev_fork2 = h->ev_fork2;
+    ws.ev_join2 = h->ev_join2;
     e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, d_diag, order,
-                                (void*)h->d_spill, h->spill_bytes, s, h->aux, h->ev_fork, h->ev_join,
-                                &h->last_kernel);
+                                (void*)h->d_spill, h->spill_bytes, s, ws, &h->last_kernel);
     if (e != hipSuccess) return hip_fail(e, "wide solve launch");
     h->last_ordered = order != nullptr;
     return record_on(h, s);

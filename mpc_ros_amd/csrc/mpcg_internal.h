@@ -22,12 +22,20 @@ size_t wide_lds_bytes(const IpmParams& P);
 // per wavefront the device holds resident (wide_slots), claimed by each problem's wavefront
 size_t wide_spill_bytes(const IpmParams& P, int64_t B);
 int64_t wide_slots(const IpmParams& P, int64_t B);
+// batches beyond the resident wavefronts are solved in expected-longest-first order
+constexpr int64_t kOrderMinBatch = 2048;
+// The streams and events a solve forks work onto (each joined back into the caller's stream
+// before the launch returns): aux -- the resume workers of the restoration phase, and the fp32
+// configuration's head (the problems the solve order ranks longest, solved in fp64 while the
+// fp32 phase runs); aux2 -- the head's own resume workers.
+struct WideStreams {
+    hipStream_t aux = nullptr, aux2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
+};
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
                              const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
-                             hipStream_t aux = nullptr,
-                             hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
-                             const char** kernel_name = nullptr);
+                             const WideStreams& ws = WideStreams(), const char** kernel_name = nullptr);
 // park-area capacity of a batch of B (problems that enter the restoration phase)
 int64_t wide_park_cap(const IpmParams& P, int64_t B);
 // Solve order (expected-longest first): device buffer bytes for B problems, and the

@@ -227,12 +227,39 @@ static size_t handoff_offset(const IpmParams& P, int64_t B) {
 static int64_t handoff_stride(const IpmParams& P) {
     return ((int64_t)(4 + 30 * P.N) + 31) / 32 * 32;  // (WideSolver::handoff_elems, whole lines)
 }
+// The fp32 configuration's head: the problems the solve order ranks longest (ordered batches only,
+// B / 1024 of them) are solved by the fp64 solver from the start on the aux stream while the fp32
+// phase runs the others -- the longest fp64 solves (through the restoration phase) would otherwise
+// start only with the fp64 phase and set its length (problem 19,304 of the infinity set at N = 40:
+// rank 2 of the order, 217 fp64 iterations, 11.5 ms alone).
+static int64_t head_count(int64_t B) {
+    int64_t div = 1024;
+#ifdef MPCG_HEAD_ENV
+    // (diagnostic builds only: the head's share of the batch, B / MPCG_HEAD_DIV; 0: no head)
+    if (const char* d = getenv("MPCG_HEAD_DIV")) div = atol(d);
+    if (div <= 0) return 0;
+#endif
+    return B > kOrderMinBatch ? B / div : 0;
+}
+static size_t order2_offset(const IpmParams& P, int64_t B) {
+    return handoff_offset(P, B) + (size_t)handoff_stride(P) * sizeof(float) * (size_t)B;
+}
+static size_t head_offset(const IpmParams& P, int64_t B) {
+    return (order2_offset(P, B) + ((size_t)(B + 63) / 64 * 64 + 64) * sizeof(int32_t) + 255) & ~(size_t)255;
+}
 size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
-    // (+ the fp64 phase's solve order: B indices and two counters)
-    if (two_phase(P))
-        return handoff_offset(P, B) + (size_t)handoff_stride(P) * sizeof(float) * (size_t)B +
-               ((size_t)(B + 63) / 64 * 64 + 64) * sizeof(int32_t);
+    // (+ the fp64 phase's solve order: B indices and two counters, + the head's workspace)
+    if (two_phase(P)) {
+        const int64_t K = head_count(B);
+        return head_offset(P, B) + (K > 0 ? phase_bytes(fp64_params(P), K) : 0);
+    }
     return phase_bytes(P, B);
+}
+
+// diag[p][2] = mark for the problems p = order[0, K)
+__global__ void __launch_bounds__(256) k_mark_rows(int64_t K, const int32_t* order, int32_t* diag, int32_t mark) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b < K) diag[(int64_t)order[b] * 4 + 2] = mark;
 }
 
 // The fp64 phase's solve order: the problems the fp32 phase did not converge on (solved from the
@@ -402,7 +429,7 @@ static WideInst warm_kernel(const IpmParams& Pr) {
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,
                              const int32_t* order, void* spill, size_t spill_bytes, hipStream_t stream,
-                             hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join, const char** kernel_name) {
+                             const WideStreams& ws, const char** kernel_name) {
     if (B <= 0) return hipSuccess;
     if (!spill) return hipErrorInvalidValue;
     if (wide_spill_bytes(P, B) > spill_bytes) return hipErrorInvalidValue;
@@ -411,27 +438,57 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     if (kernel_name) *kernel_name = inst.name;
     if (!two_phase(P))
         return launch_phase(P, inst, B, state, coeffs, u0, traj, status, obj, iters, diag, order, spill, nullptr,
-                            stream, aux, ev_fork, ev_join);
-    // the fp32 configuration: the fp32 phase (hand-over, no outputs), then the fp64 phase
-    float* handoff = (float*)((char*)spill + handoff_offset(P, B));
-    hipError_t e = launch_phase(P, inst, B, state, coeffs, u0, traj, status, obj, iters, diag, order, spill, handoff,
-                                stream, aux, ev_fork, ev_join);
-    if (e != hipSuccess) return e;
+                            stream, ws.aux, ws.ev_fork, ws.ev_join);
+    // the fp32 configuration: [the head on aux, in fp64 from the start] the fp32 phase (hand-over,
+    // no outputs), then the fp64 phase, over the problems outside the head
     IpmParams Pr = fp64_params(P);
+    const bool can_head = order && ws.aux && ws.aux != stream && ws.aux2 && ws.aux2 != ws.aux && ws.ev_fork &&
+                          ws.ev_join && ws.ev_fork2 && ws.ev_join2;
+    const int64_t K = can_head ? head_count(B) : 0;
+    hipError_t e;
+    if (K > 0) {
+        // (after the solve order: the head is order[0, K); its workspace is its own, its resume
+        // workers fork onto aux2 and join back into aux)
+        e = hipEventRecord(ws.ev_fork, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ws.aux, ws.ev_fork, 0);
+        if (e != hipSuccess) return e;
+        const WideInst hi = wide_kernel(Pr, B);  // (the fp64 solver's batch instance)
+        if (!hi.fn) return hipErrorInvalidValue;
+        e = launch_phase(Pr, hi, K, state, coeffs, u0, traj, status, obj, iters, diag, order,
+                         (char*)spill + head_offset(P, B), nullptr, ws.aux, ws.aux2, ws.ev_fork2, ws.ev_join2);
+        if (e != hipSuccess) return e;
+        if (diag) {  // (solved from the start by the fp64 solver: diag[:, 2] = 3, after the head's last write)
+            hipLaunchKernelGGL(k_mark_rows, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, ws.aux, K, order, diag, 3);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    const int64_t Bm = B - K;
+    const int32_t* om = order ? order + K : nullptr;
+    float* handoff = (float*)((char*)spill + handoff_offset(P, B));
+    e = launch_phase(P, inst, Bm, state, coeffs, u0, traj, status, obj, iters, diag, om, spill, handoff, stream,
+                     ws.aux, ws.ev_fork, ws.ev_join);
+    if (e != hipSuccess) return e;
     const WideInst wi = warm_kernel(Pr);
-    int32_t* order2 = (int32_t*)(handoff + (size_t)handoff_stride(P) * (size_t)B);
+    int32_t* order2 = (int32_t*)((char*)spill + order2_offset(P, B));
     int32_t* cnt2 = order2 + ((B + 63) / 64) * 64;
     hipLaunchKernelGGL(k_reset_ws, dim3(1), dim3(256), 0, stream, cnt2, (int64_t)0, cnt2, nullptr, (int64_t)0,
                        nullptr, (int64_t)0);
-    hipLaunchKernelGGL(k_cold_first, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream, B, (const float*)handoff,
-                       handoff_stride(P), order, order2, cnt2);
+    hipLaunchKernelGGL(k_cold_first, dim3((unsigned)((Bm + 255) / 256)), dim3(256), 0, stream, Bm,
+                       (const float*)handoff, handoff_stride(P), om, order2, cnt2);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // (the problems solved from the start come first and some of them enter the restoration
     // phase early in the launch: more concurrent resume workers than a batch of the fp64 solver
     // needs, so they are continued while the rest of the batch runs)
-    return launch_phase(Pr, wi, B, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
-                        aux, ev_fork, ev_join, 8 + B / 2048);
+    e = launch_phase(Pr, wi, Bm, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
+                     ws.aux, ws.ev_fork, ws.ev_join, 8 + B / 2048);
+    if (e != hipSuccess) return e;
+    if (K > 0) {  // (the head, whatever the fp64 phase forked)
+        e = hipEventRecord(ws.ev_join, ws.aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ws.ev_join, 0);
+    }
+    return e;
 }
 
 }  // namespace mpcg

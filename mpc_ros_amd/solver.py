@@ -26,6 +26,8 @@ IPOPT_DEFAULTS = dict(tol=1e-8, max_iter=3000, filter_cap=64, bound_relax_factor
 #     tolerance, diag[:, 2] == 4), else from the start (its line search failed at a float
 #     iterate's noise floor where Ipopt would enter the restoration phase, a tiny step, the
 #     iteration limit: diag[:, 2] == 3, bitwise the fp64 solver's result).
+# (B > 2048: the B / 1024 problems the solve order ranks longest are solved by the fp64 solver from
+# the start, diag[:, 2] == 3, while the fp32 phase runs the others.)
 # The returned controls are the fp64 solver's (within 1e-6 of the reference's double-precision
 # solve where they converge to the same local minimum).  no_restoration = 1 runs the fp32 phase
 # alone and keeps its ending (status 9, 3 or 2 where it cannot finish).

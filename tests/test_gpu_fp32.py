@@ -103,8 +103,10 @@ def test_fp32_full_batch_against_fp64(torch_cuda):
 def test_fp32_no_restoration_option(torch_cuda):
     """no_restoration = 1: the fp32 phase alone, its own ending kept -- status 9 where Ipopt
     would restore, 3 at a tiny step, 2 at the iteration limit on exactly the rows the two-phase
-    solve takes from the start in fp64; the other rows converge in fp32 (status 1 or 4) to within
-    the float solver's accuracy of the two-phase result."""
+    solve takes from the start in fp64 (but the head: the B / 1024 rows the solve order ranks
+    longest, solved in fp64 from the start while the fp32 phase runs, whatever their fp32 ending
+    would be); the other rows converge in fp32 (status 1 or 4) to within the float solver's
+    accuracy of the two-phase result."""
     from mpc_ros_amd import infinity, params
     from mpc_ros_amd.solver import BatchSolver
 
@@ -113,7 +115,8 @@ def test_fp32_no_restoration_option(torch_cuda):
     a = BatchSolver(0, P, dtype="fp32").solve(st, cf)
     b = BatchSolver(0, P, dtype="fp32", no_restoration=1).solve(st, cf)
     cold = a["diag"][:, 2] == 3
-    assert cold.any() and (b["diag"][:, 2] == 0).all() and np.isin(b["status"][cold], (2, 3, 9)).all()
+    assert cold.any() and (b["diag"][:, 2] == 0).all()
+    assert (cold & ~np.isin(b["status"], (2, 3, 9))).sum() <= 4096 // 1024  # (the head)
     assert np.isin(b["status"][~cold], (1, 4)).all()
     assert np.abs(a["u0"][~cold] - b["u0"][~cold]).max() <= 1e-2
 
