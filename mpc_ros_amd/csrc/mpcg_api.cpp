@@ -40,7 +40,7 @@ struct mpcg_handle {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // (the fp32 configuration's head runs on aux, its resume workers on aux2)
     hipStream_t aux2 = nullptr;
-    hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
+    hipEvent_t ev_join2 = nullptr;
     mpcg_params params{};
     // staging buffers for mpcg_solve (host pointers)
     double* d_io = nullptr;
@@ -326,7 +326,6 @@ int mpcg_create(int device, mpcg_handle** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join2, hipEventDisableTiming);
     if (e != hipSuccess) {
         mpcg_destroy(h);
@@ -352,7 +351,6 @@ void mpcg_destroy(mpcg_handle* h) {
     if (h->last_ev) hipEventDestroy(h->last_ev);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
-    if (h->ev_fork2) hipEventDestroy(h->ev_fork2);
     if (h->ev_join2) hipEventDestroy(h->ev_join2);
     if (h->aux) hipStreamDestroy(h->aux);
     if (h->aux2) hipStreamDestroy(h->aux2);
@@ -499,7 +497,6 @@ int mpcg_solve_device_ex(mpcg_handle* h, int64_t B, const double* d_state, const
     ws.aux2 = h->aux2;
     ws.ev_fork = h->ev_fork;
     ws.ev_join = h->ev_join;
-    ws.ev_fork2 = h->ev_fork2;
     ws.ev_join2 = h->ev_join2;
     e = mpcg::launch_wide_solve(P, B, d_state, d_coeffs, d_u0, d_traj, d_status, d_obj, d_iters, d_diag, order,
                                 (void*)h->d_spill, h->spill_bytes, s, ws, &h->last_kernel);

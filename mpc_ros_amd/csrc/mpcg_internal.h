@@ -30,7 +30,7 @@ constexpr int64_t kOrderMinBatch = 2048;
 // fp32 phase runs); aux2 -- the head's own resume workers.
 struct WideStreams {
     hipStream_t aux = nullptr, aux2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
 };
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,
                              double* traj, int32_t* status, double* obj, int32_t* iters, int32_t* diag,

@@ -244,6 +244,13 @@ static int64_t head_count(int64_t B) {
 static size_t order2_offset(const IpmParams& P, int64_t B) {
     return handoff_offset(P, B) + (size_t)handoff_stride(P) * sizeof(float) * (size_t)B;
 }
+// the head's parameters: the fp64 solver's, with a park entry for every head problem (no
+// park-area overflow: the head's stream never waits for its resume workers' stream)
+static IpmParams head_params(const IpmParams& P, int64_t K) {
+    IpmParams q = fp64_params(P);
+    q.park_cap = (int)K;
+    return q;
+}
 static size_t head_offset(const IpmParams& P, int64_t B) {
     return (order2_offset(P, B) + ((size_t)(B + 63) / 64 * 64 + 64) * sizeof(int32_t) + 255) & ~(size_t)255;
 }
@@ -251,7 +258,7 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
     // (+ the fp64 phase's solve order: B indices and two counters, + the head's workspace)
     if (two_phase(P)) {
         const int64_t K = head_count(B);
-        return head_offset(P, B) + (K > 0 ? phase_bytes(fp64_params(P), K) : 0);
+        return head_offset(P, B) + (K > 0 ? phase_bytes(head_params(P, K), K) : 0);
     }
     return phase_bytes(P, B);
 }
@@ -296,11 +303,17 @@ static int64_t resume_workers(int64_t B) {
 // One batch launch (with its resume workers, drain and overflow launches) of the instance inst
 // for parameters P on the workspace at spill.  handoff: the fp32 configuration's hand-over
 // buffer (the fp32 phase writes it, the fp64 phase -- inst a k_warm_wide instance -- reads it).
+// origin (the fp32 configuration's head): &the caller's stream (a pointer: the caller's stream may
+// be the null stream) -- the workspace reset runs there,
+// then both `stream` and (with workers) `aux` fork from it (ev_fork), and the caller joins them
+// (*forked_out: whether aux received work); no stream forks from a forked stream, which a
+// captured graph does not survive.
 static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t B, const double* state,
                                const double* coeffs, double* u0, double* traj, int32_t* status, double* obj,
                                int32_t* iters, int32_t* diag, const int32_t* order, void* spill, float* handoff,
                                hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join,
-                               int64_t nworkers = -1) {
+                               int64_t nworkers = -1, const hipStream_t* origin = nullptr,
+                               bool* forked_out = nullptr) {
     size_t lds = wide_lds_bytes(P);
 #ifdef MPCG_LDS_PAD_ENV
     // (diagnostic builds only: extra LDS per workgroup, fewer problems per CU)
@@ -353,9 +366,14 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
         int64_t n = npr > 64 ? npr : 64;
         n = n > nov ? n : nov;
         n = n > ns ? n : ns;
-        hipLaunchKernelGGL(k_reset_ws, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, flags, ns, cnt,
-                           pready, npr, ovf, nov);
+        hipLaunchKernelGGL(k_reset_ws, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, origin ? *origin : stream,
+                           flags, ns, cnt, pready, npr, ovf, nov);
         e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (origin) {
+        e = hipEventRecord(ev_fork, *origin);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_fork, 0);
         if (e != hipSuccess) return e;
     }
     WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
@@ -380,8 +398,9 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
     const bool can_fork = B > 1 && aux && aux != stream && ev_fork && ev_join;
     const unsigned workers = can_fork ? (unsigned)(pc < nw ? pc : nw) : 0u;
     const bool fork = workers > 0;
+    if (forked_out) *forked_out = fork;
     if (fork) {
-        e = hipEventRecord(ev_fork, stream);
+        e = origin ? hipSuccess : hipEventRecord(ev_fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);
         if (e != hipSuccess) return e;
     }
@@ -396,7 +415,7 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
     // -- the tail is the longest restoration, not their sum over a few workers
     e = hipLaunchKernel(rf, dim3((unsigned)pc), dim3(64), args, rlds, stream);
     if (e != hipSuccess) return e;
-    if (fork) {
+    if (fork && !origin) {
         e = hipEventRecord(ev_join, aux);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
         if (e != hipSuccess) return e;
@@ -442,26 +461,22 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     // the fp32 configuration: [the head on aux, in fp64 from the start] the fp32 phase (hand-over,
     // no outputs), then the fp64 phase, over the problems outside the head
     IpmParams Pr = fp64_params(P);
-    const bool can_head = order && ws.aux && ws.aux != stream && ws.aux2 && ws.aux2 != ws.aux && ws.ev_fork &&
-                          ws.ev_join && ws.ev_fork2 && ws.ev_join2;
+    const bool can_head = order && ws.aux && ws.aux != stream && ws.aux2 && ws.aux2 != ws.aux &&
+                          ws.aux2 != stream && ws.ev_fork && ws.ev_join && ws.ev_join2;
     const int64_t K = can_head ? head_count(B) : 0;
     hipError_t e;
+    bool head_workers = false;
     if (K > 0) {
-        // (after the solve order: the head is order[0, K); its workspace is its own, its resume
-        // workers fork onto aux2 and join back into aux)
-        e = hipEventRecord(ws.ev_fork, stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ws.aux, ws.ev_fork, 0);
-        if (e != hipSuccess) return e;
-        const WideInst hi = wide_kernel(Pr, B);  // (the fp64 solver's batch instance)
+        // (after the solve order: the head is order[0, K), on its own workspace; aux and the
+        // head's resume workers on aux2 both fork from the caller's stream -- no fork of a forked
+        // stream, which a captured graph does not survive -- and both join it after the fp32 phase)
+        const IpmParams Ph = head_params(P, K);
+        const WideInst hi = wide_kernel(Ph, B);  // (the fp64 solver's batch instance)
         if (!hi.fn) return hipErrorInvalidValue;
-        e = launch_phase(Pr, hi, K, state, coeffs, u0, traj, status, obj, iters, diag, order,
-                         (char*)spill + head_offset(P, B), nullptr, ws.aux, ws.aux2, ws.ev_fork2, ws.ev_join2);
+        e = launch_phase(Ph, hi, K, state, coeffs, u0, traj, status, obj, iters, diag, order,
+                         (char*)spill + head_offset(P, B), nullptr, ws.aux, ws.aux2, ws.ev_fork, ws.ev_join2, -1,
+                         &stream, &head_workers);
         if (e != hipSuccess) return e;
-        if (diag) {  // (solved from the start by the fp64 solver: diag[:, 2] = 3, after the head's last write)
-            hipLaunchKernelGGL(k_mark_rows, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, ws.aux, K, order, diag, 3);
-            e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
     }
     const int64_t Bm = B - K;
     const int32_t* om = order ? order + K : nullptr;
@@ -469,6 +484,21 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     e = launch_phase(P, inst, Bm, state, coeffs, u0, traj, status, obj, iters, diag, om, spill, handoff, stream,
                      ws.aux, ws.ev_fork, ws.ev_join);
     if (e != hipSuccess) return e;
+    if (K > 0) {  // (the head joins before the fp64 phase forks its own workers onto aux)
+        if (head_workers) {
+            e = hipEventRecord(ws.ev_join2, ws.aux2);
+            if (e == hipSuccess) e = hipStreamWaitEvent(stream, ws.ev_join2, 0);
+            if (e != hipSuccess) return e;
+        }
+        e = hipEventRecord(ws.ev_join, ws.aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ws.ev_join, 0);
+        if (e != hipSuccess) return e;
+        if (diag) {  // (solved from the start by the fp64 solver: diag[:, 2] = 3, after the head's last write)
+            hipLaunchKernelGGL(k_mark_rows, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, K, order, diag, 3);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
     const WideInst wi = warm_kernel(Pr);
     int32_t* order2 = (int32_t*)((char*)spill + order2_offset(P, B));
     int32_t* cnt2 = order2 + ((B + 63) / 64) * 64;
@@ -481,14 +511,8 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     // (the problems solved from the start come first and some of them enter the restoration
     // phase early in the launch: more concurrent resume workers than a batch of the fp64 solver
     // needs, so they are continued while the rest of the batch runs)
-    e = launch_phase(Pr, wi, Bm, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
-                     ws.aux, ws.ev_fork, ws.ev_join, 8 + B / 2048);
-    if (e != hipSuccess) return e;
-    if (K > 0) {  // (the head, whatever the fp64 phase forked)
-        e = hipEventRecord(ws.ev_join, ws.aux);
-        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ws.ev_join, 0);
-    }
-    return e;
+    return launch_phase(Pr, wi, Bm, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
+                        ws.aux, ws.ev_fork, ws.ev_join, 8 + B / 2048);
 }
 
 }  // namespace mpcg

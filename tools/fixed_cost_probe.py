@@ -1,6 +1,6 @@
 """Diagnostic: a solve's fixed cost against its per-iteration cost (B = 65,536, N = 20 by default).
 
-    python tools/fixed_cost_probe.py [N] [B]
+    python tools/fixed_cost_probe.py [N] [B] [bicycle]
 
 Times the batch with max_iter = 0, 1, 2, 4, 8 and the reference's options (the iteration budget
 stops every problem at that count; max_iter = 0 is set-up, the starting point, the least-squares
@@ -16,6 +16,8 @@ from mpc_ros_amd.solver import BatchSolver  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 P = dict(params.PLUGIN_DEFAULTS, STEPS=N)
+if len(sys.argv) > 3 and sys.argv[3] == "bicycle":  # (bench.py's bicycle configuration)
+    P.update(MODEL=1, LF=0.5, ANGVEL=0.5)
 dev = torch.device("cuda:0")
 for mi in (0, 1, 2, 4, 8, None):
     s = BatchSolver(0, P) if mi is None else BatchSolver(0, P, max_iter=mi)
