@@ -188,9 +188,11 @@ int mpcg_solve(mpcg_handle* h, int64_t B, const double* state, const double* coe
 
 /* Batched solve on device-resident buffers (same layouts), queued on `stream` (a
  * hipStream_t; NULL = the null stream, as everywhere in HIP) without any host
- * synchronisation: the whole solve is one kernel (plus the solve-order sort for
- * B > 2048).  Synchronise the stream before reading the outputs on the host.  No
- * allocation if mpcg_reserve(h, B) was called. */
+ * synchronisation: the solve-order sort (B > 2048), a workspace reset, the batch kernel and
+ * the restoration phase's resume kernels; work forked onto the handle's own streams (resume
+ * workers, the fp32 configuration's head) is joined back into `stream` by events, so the
+ * sequence can be captured in a HIP graph.  Synchronise the stream before reading the outputs
+ * on the host.  No allocation if mpcg_reserve(h, B) was called. */
 int mpcg_solve_device(mpcg_handle* h, int64_t B, const double* d_state, const double* d_coeffs, double* d_u0,
                       double* d_traj, int32_t* d_status, double* d_obj, int32_t* d_iters, void* stream);
 
