@@ -435,6 +435,10 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
 
 // the fp64 phase's instance (k_warm_wide, default options) for the horizon class of P
 static WideInst warm_kernel(const IpmParams& Pr) {
+#ifdef MPCG_HEADLINE_ONLY
+    (void)Pr;
+    return WideInst{nullptr, ""};  // (not linked into the timing tool)
+#else
     const bool split = Pr.N <= 32;
     const int nb = Pr.N > 64 ? 2 : 1;
     if (Pr.N > 128 || Pr.model != 0) return WideInst{nullptr, ""};
@@ -443,6 +447,7 @@ static WideInst warm_kernel(const IpmParams& Pr) {
     if (wide_lds_bytes(Pr) > 32768)
         return WideInst{warm_kernel_fn<0, false, double, 1, true, 1>(), "k_warm_wide<0,false,double,1,true,1>"};
     return WideInst{warm_kernel_fn<0, false, double, 1, true, 2>(), "k_warm_wide<0,false,double,1,true,2>"};
+#endif
 }
 
 hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state, const double* coeffs, double* u0,

@@ -85,8 +85,12 @@ int main(int argc, char** argv) {
 #ifdef WT_OLD_API
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, order, dspill, 0));
 #else
+        mpcg::WideStreams ws;
+        ws.aux = getenv("WT_SEQ") ? nullptr : aux;
+        ws.ev_fork = evf;
+        ws.ev_join = evj;
         CK(mpcg::launch_wide_solve(P, B, dst, dcf, du0, nullptr, dss, dobj, dit, nullptr, order, dspill,
-                                   mpcg::wide_spill_bytes(P, B), 0, getenv("WT_SEQ") ? nullptr : aux, evf, evj));
+                                   mpcg::wide_spill_bytes(P, B), 0, ws));
 #endif
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
