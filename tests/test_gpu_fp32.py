@@ -290,3 +290,24 @@ def test_fp32_repeated_solves_on_the_default_stream(torch_cuda):
         np.testing.assert_array_equal(status.cpu().numpy(), ref["status"])
         np.testing.assert_array_equal(iters.cpu().numpy(), ref["iters"])
         np.testing.assert_array_equal(u0.cpu().numpy(), ref["u0"])
+
+
+def test_fp32_multi_context_matches_single(torch_cuda):
+    """The fp32 configuration through the persistent multi-GPU context (each GPU's handle solves
+    its shard on its own stream: the head forks from that stream) equals the single-handle solve
+    bitwise, with and without the head (B = 4,096 and 2,048)."""
+    torch = torch_cuda
+    from mpc_ros_amd import infinity, params
+    from mpc_ros_amd.solver import BatchSolver, MultiSolver
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=40)
+    st, cf = infinity.make_problems(np.arange(4096))
+    devs = list(range(torch.cuda.device_count()))
+    m = MultiSolver(devs, 4096, P, dtype="fp32")
+    s = BatchSolver(0, P, dtype="fp32")
+    for B in (4096, 2048):
+        r = m.solve(st[:B], cf[:B])
+        ref = s.solve(st[:B], cf[:B])
+        for k in ("u0", "traj", "status", "iters", "obj"):
+            np.testing.assert_array_equal(r[k], ref[k])
+    m.close()
