@@ -8,6 +8,6 @@ for c in ${CFGS:-n40 bic25}; do
     MPCG_RESUME_WORKERS=$w timeout -k 10 300 python bench.py --steps ${CSTEPS:-6} --warmup 2 --cpu-seconds 0 $a > $O/${c}_w$w.log 2>&1; rc=$?
     [ $rc -eq 0 ] || { echo "$c w$w rc=$rc"; exit 1; }
     tail -1 $O/${c}_w$w.log > $O/${c}_w$w.json
-    python3 -c "import json; d=json.load(open('$O/${c}_w$w.json')); print('$c w$w', round(d['value']), round(d['timing']['kernel_ms'],2))"
+    python3 -c "import json; d=json.load(open('$O/${c}_w$w.json')); print('$c w$w', round(d['value']), round(d['ms_per_step'],2))"
   done
 done
