@@ -112,6 +112,14 @@ def test_workspace_bytes(libmpcg):
     assert big < 65536 * 3184 * 8 // 4  # (bounded by residency, not by B)
     assert libmpcg.mpcg_workspace_bytes(C.byref(p), 0) == 0
     assert libmpcg.mpcg_handle_workspace_bytes(None, 1) == 0  # (no handle: nothing)
+    # the fp32 configuration: + the hand-over (4 + 30N floats per problem in whole 128-byte
+    # lines: 608 at N = 20), the fp64 phase's order and, beyond 2048 problems, the head's own
+    # workspace (B / 1024 problems of the fp64 solver, a park entry each)
+    p.precision = 1
+    w2048 = libmpcg.mpcg_workspace_bytes(C.byref(p), 2048)
+    w2049 = libmpcg.mpcg_workspace_bytes(C.byref(p), 2049)
+    assert w2048 >= 2048 * 608 * 4
+    assert w2049 - w2048 >= 608 * 4 + 2 * 14096 * 8  # (one more hand-over row, the head's park entries)
     assert libmpcg.mpcg_last_solve_order(None) == 0
 
 
