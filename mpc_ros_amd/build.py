@@ -127,7 +127,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     return LIB
 
 
-RESOURCES = os.path.join(ROOT, "profiles", "r5", "resources.json")
+RESOURCES = os.path.join(ROOT, "profiles", "r6", "resources.json")
 
 
 def demangle(names):

@@ -9,8 +9,11 @@
 // rank r sends its shard, the root receives every shard at its offset -- point-to-point
 // over xGMI, the north star's "RCCL used only for the final gather"), then copied to the
 // caller's host buffers.  The context holds the communicator, a handle, stream and device
-// buffers per GPU, and each handle's solver workspace reserved for the largest shard: a
-// solve allocates nothing.  Every HIP and RCCL return is checked; a failure sets
+// buffers per GPU, pinned host staging for the inputs of each shard and the root's outputs,
+// and each handle's solver workspace reserved for the largest shard: a solve allocates
+// nothing.  The shards' inputs are staged and their copies and solves queued by one host
+// thread per GPU, so no GPU waits for another's host-to-device copy (a copy from the caller's
+// pageable memory returns only once it has completed).  Every HIP and RCCL return is checked; a failure sets
 // mpcg_last_error(); a failure inside the gather group aborts the communicators (an
 // unmatched send must not be waited for) and marks the context broken.
 #include <hip/hip_runtime.h>
@@ -18,6 +21,7 @@
 
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mpcg.h"
@@ -31,6 +35,8 @@ struct Shard {
     int64_t start = 0, count = 0;
     double* in = nullptr;   // state [count][6] | coeffs [count][4]
     char* out = nullptr;    // root: gathered outputs of all B problems; others: their shard
+    double* hin = nullptr;  // pinned host staging of `in` (the largest shard)
+    char* hout = nullptr;   // root only: pinned host staging of the gathered outputs
 };
 
 // output record layout of B problems: u0 [B][2] | traj [B][3N] | obj [B] | status [B] | iters [B]
@@ -126,6 +132,8 @@ void multi_free(mpcg_multi* m) {
         if (s.h) mpcg_destroy(s.h);
         if (s.in) hipFree(s.in);
         if (s.out) hipFree(s.out);
+        if (s.hin) hipHostFree(s.hin);
+        if (s.hout) hipHostFree(s.hout);
         if (s.s) hipStreamDestroy(s.s);
         s = Shard{};
     }
@@ -182,6 +190,11 @@ int mpcg_multi_create(int ngpu, const int* devices, const mpcg_params* params, i
                 result = hip_fail(he, "hipMalloc");
                 break;
             }
+            if ((he = hipHostMalloc((void**)&s.hin, in_bytes, hipHostMallocDefault)) != hipSuccess ||
+                (r == 0 && (he = hipHostMalloc((void**)&s.hout, out_bytes, hipHostMallocDefault)) != hipSuccess)) {
+                result = hip_fail(he, "hipHostMalloc");
+                break;
+            }
         }
     } while (false);
     if (result) {
@@ -211,26 +224,43 @@ int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double
     for (int r = 0; r < ngpu; ++r) mpcg_shard_range(B, ngpu, r, &sh[r].start, &sh[r].count);
     hipError_t he;
     int rc;
-    // shards: copy in, solve (each on its own GPU and stream, queued without waiting)
-    for (int r = 0; r < ngpu; ++r) {
+    // shards: stage the inputs in pinned memory, copy in, solve -- one host thread per GPU, so
+    // each GPU's copy and solve are queued without waiting for another GPU's copy
+    auto enqueue = [&](int r) -> int {
         Shard& s = sh[r];
-        if (s.count == 0) continue;
-        if ((he = hipSetDevice(s.dev)) != hipSuccess) return hip_fail(he, "hipSetDevice");
+        if (s.count == 0) return 0;
+        hipError_t e;
+        if ((e = hipSetDevice(s.dev)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+        std::memcpy(s.hin, state + 6 * s.start, sizeof(double) * 6 * s.count);
+        std::memcpy(s.hin + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count);
         double* din = s.in;
-        if ((he = hipMemcpyAsync(din, state + 6 * s.start, sizeof(double) * 6 * s.count, hipMemcpyHostToDevice,
-                                 s.s)) != hipSuccess ||
-            (he = hipMemcpyAsync(din + 6 * s.count, coeffs + 4 * s.start, sizeof(double) * 4 * s.count,
-                                 hipMemcpyHostToDevice, s.s)) != hipSuccess)
-            return hip_fail(he, "hipMemcpyAsync (inputs)");
+        if ((e = hipMemcpyAsync(din, s.hin, sizeof(double) * 10 * s.count, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync (inputs)");
         // the root solves into its own slot of the gathered arrays (the plan's src offsets)
         mpcg_xfer x[MPCG_GATHER_ARRAYS];
-        if ((rc = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) return rc;
+        int c;
+        if ((c = mpcg_multi_gather_plan(B, N, ngpu, r, x)) != 0) return c;
         char* o = s.out;
-        rc = mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + x[0].src_offset),
-                               (double*)(o + x[1].src_offset), (int32_t*)(o + x[3].src_offset),
-                               (double*)(o + x[2].src_offset), (int32_t*)(o + x[4].src_offset), s.s);
-        if (rc) return rc;
+        return mpcg_solve_device(s.h, s.count, din, din + 6 * s.count, (double*)(o + x[0].src_offset),
+                                 (double*)(o + x[1].src_offset), (int32_t*)(o + x[3].src_offset),
+                                 (double*)(o + x[2].src_offset), (int32_t*)(o + x[4].src_offset), s.s);
+    };
+    std::vector<int> rcs(ngpu, 0);
+    std::vector<std::string> errs(ngpu);
+    if (ngpu == 1) {
+        rcs[0] = enqueue(0);
+    } else {
+        // (mpcg_last_error() is per thread: a worker's message is carried back)
+        std::vector<std::thread> th;
+        for (int r = 0; r < ngpu; ++r)
+            th.emplace_back([&, r] {
+                rcs[r] = enqueue(r);
+                if (rcs[r]) errs[r] = mpcg_last_error();
+            });
+        for (auto& t : th) t.join();
     }
+    for (int r = 0; r < ngpu; ++r)
+        if (rcs[r]) return ngpu == 1 ? rcs[r] : mpcg::set_error(rcs[r], errs[r]);
     // the gather: rank r > 0 sends each of its output arrays, the root receives them at their
     // offsets (grouped point-to-point: every shard moves once over xGMI).  The plan is checked
     // before the group opens; a failing call inside it closes the group (not launched: it has a
@@ -265,7 +295,7 @@ int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double
         for (auto& c : m->comms) ncclCommAbort(c), c = nullptr;
         return nccl_fail(ne, "ncclGroupEnd");
     }
-    // results to the host from the root
+    // results to the host from the root, through its pinned staging
     if ((he = hipSetDevice(sh[0].dev)) != hipSuccess) return hip_fail(he, "hipSetDevice");
     const OutLayout G{B, N};
     const char* o = sh[0].out;
@@ -276,12 +306,14 @@ int mpcg_multi_solve(mpcg_multi* m, int64_t B, const double* state, const double
         {iters, G.iters(), sizeof(int32_t) * B}};
     for (const auto& b : back) {
         if (!b.host) continue;
-        if ((he = hipMemcpyAsync(b.host, o + b.off, b.bytes, hipMemcpyDeviceToHost, s0)) != hipSuccess)
+        if ((he = hipMemcpyAsync(sh[0].hout + b.off, o + b.off, b.bytes, hipMemcpyDeviceToHost, s0)) != hipSuccess)
             return hip_fail(he, "hipMemcpyAsync (results)");
     }
     for (auto& s : sh)
         if ((he = hipSetDevice(s.dev)) != hipSuccess || (he = hipStreamSynchronize(s.s)) != hipSuccess)
             return hip_fail(he, "hipStreamSynchronize");
+    for (const auto& b : back)
+        if (b.host) std::memcpy(b.host, sh[0].hout + b.off, b.bytes);
     return 0;
 }
 

@@ -263,10 +263,14 @@ size_t wide_spill_bytes(const IpmParams& P, int64_t B) {
     return phase_bytes(P, B);
 }
 
-// diag[p][2] = mark for the problems p = order[0, K)
-__global__ void __launch_bounds__(256) k_mark_rows(int64_t K, const int32_t* order, int32_t* diag, int32_t mark) {
+// diag[p][2] = mark for the problems p = order[0, K) (of n_prob)
+__global__ void __launch_bounds__(256) k_mark_rows(int64_t K, const int32_t* order, int32_t* diag, int32_t mark,
+                                                   int64_t n_prob) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b < K) diag[(int64_t)order[b] * 4 + 2] = mark;
+    if (b >= K) return;
+    const int64_t p = order[b];
+    check_index("head order: problem", p, n_prob);
+    diag[p * 4 + 2] = mark;
 }
 
 // The fp64 phase's solve order: the problems the fp32 phase did not converge on (solved from the
@@ -274,10 +278,11 @@ __global__ void __launch_bounds__(256) k_mark_rows(int64_t K, const int32_t* ord
 // few fp64 iterations each), so the long solves do not trail the batch.  Positions by two atomic
 // counters (from the front, and from the back): results do not depend on the order.
 __global__ void __launch_bounds__(256) k_cold_first(int64_t B, const float* h, int64_t stride, const int32_t* order,
-                                                    int32_t* out, int32_t* cnt) {
+                                                    int32_t* out, int32_t* cnt, int64_t n_prob) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (b >= B) return;
     const int32_t p = order ? order[b] : (int32_t)b;
+    check_index("fp64 phase order: problem", p, n_prob);
     if (h[(int64_t)p * stride] != 0.0f)
         out[B - 1 - atomicAdd(&cnt[1], 1)] = p;
     else
@@ -313,7 +318,7 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
                                int32_t* iters, int32_t* diag, const int32_t* order, void* spill, float* handoff,
                                hipStream_t stream, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join,
                                int64_t nworkers = -1, const hipStream_t* origin = nullptr,
-                               bool* forked_out = nullptr) {
+                               bool* forked_out = nullptr, int64_t n_prob = -1) {
     size_t lds = wide_lds_bytes(P);
 #ifdef MPCG_LDS_PAD_ENV
     // (diagnostic builds only: extra LDS per workgroup, fewer problems per CU)
@@ -376,7 +381,8 @@ static hipError_t launch_phase(const IpmParams& P, const WideInst& inst, int64_t
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_fork, 0);
         if (e != hipSuccess) return e;
     }
-    WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag, slots, flags,
+    WideArgs a{P,      B,          order,      state,  coeffs, u0,  traj, status, obj, iters, diag,
+               n_prob > 0 ? n_prob : B, slots, flags,
                (int32_t)ns, (int32_t)slot_elems(P), cnt, fp32_phase ? 0 : (int32_t)pc, pidx, pready, cnt + 1, cnt + 2,
                park, (int64_t)park_elems(P), cnt + 3, cnt + 4, cnt + 5, ovf, (int32_t)device_xccs(), 0, 0, 2,
                handoff, handoff ? handoff_stride(P) : 0};
@@ -480,14 +486,14 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
         if (!hi.fn) return hipErrorInvalidValue;
         e = launch_phase(Ph, hi, K, state, coeffs, u0, traj, status, obj, iters, diag, order,
                          (char*)spill + head_offset(P, B), nullptr, ws.aux, ws.aux2, ws.ev_fork, ws.ev_join2, -1,
-                         &stream, &head_workers);
+                         &stream, &head_workers, B);
         if (e != hipSuccess) return e;
     }
     const int64_t Bm = B - K;
     const int32_t* om = order ? order + K : nullptr;
     float* handoff = (float*)((char*)spill + handoff_offset(P, B));
     e = launch_phase(P, inst, Bm, state, coeffs, u0, traj, status, obj, iters, diag, om, spill, handoff, stream,
-                     ws.aux, ws.ev_fork, ws.ev_join);
+                     ws.aux, ws.ev_fork, ws.ev_join, -1, nullptr, nullptr, B);
     if (e != hipSuccess) return e;
     if (K > 0) {  // (the head joins before the fp64 phase forks its own workers onto aux)
         if (head_workers) {
@@ -499,7 +505,7 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, ws.ev_join, 0);
         if (e != hipSuccess) return e;
         if (diag) {  // (solved from the start by the fp64 solver: diag[:, 2] = 3, after the head's last write)
-            hipLaunchKernelGGL(k_mark_rows, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, K, order, diag, 3);
+            hipLaunchKernelGGL(k_mark_rows, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, K, order, diag, 3, B);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -510,14 +516,14 @@ hipError_t launch_wide_solve(const IpmParams& P, int64_t B, const double* state,
     hipLaunchKernelGGL(k_reset_ws, dim3(1), dim3(256), 0, stream, cnt2, (int64_t)0, cnt2, nullptr, (int64_t)0,
                        nullptr, (int64_t)0);
     hipLaunchKernelGGL(k_cold_first, dim3((unsigned)((Bm + 255) / 256)), dim3(256), 0, stream, Bm,
-                       (const float*)handoff, handoff_stride(P), om, order2, cnt2);
+                       (const float*)handoff, handoff_stride(P), om, order2, cnt2, B);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // (the problems solved from the start come first and some of them enter the restoration
     // phase early in the launch: more concurrent resume workers than a batch of the fp64 solver
     // needs, so they are continued while the rest of the batch runs)
     return launch_phase(Pr, wi, Bm, state, coeffs, u0, traj, status, obj, iters, diag, order2, spill, handoff, stream,
-                        ws.aux, ws.ev_fork, ws.ev_join, 8 + B / 2048);
+                        ws.aux, ws.ev_fork, ws.ev_join, 8 + B / 2048, nullptr, nullptr, B);
 }
 
 }  // namespace mpcg

@@ -30,6 +30,7 @@ struct WideArgs {
     double* obj;
     int32_t* iters;
     int32_t* diag;         // [B][4] restoration phases, filter overflows, parked (1) / re-solved (2), filter peak (or null)
+    int64_t n_prob;        // problems in state / coeffs / the outputs (the caller's batch; B is this launch's share)
     void* slots;           // nslots workspaces of slot_elems elements of T (the rare paths' copies)
     int32_t* slot_flags;   // 1 while a resident wavefront holds the slot
     int32_t nslots;        // nxcc partitions of nslots / nxcc slots, one per XCD
@@ -62,6 +63,26 @@ struct WideArgs {
     float* handoff;
     int64_t handoff_stride;
 };
+// Always-on range checks of the indices a kernel reads from device memory (the solve order, the
+// park area's problem indices, the overflow list, a parked entry's counts) or derives from the
+// workspace's counters (slot, park entry): a value out of range is reported and the kernel
+// traps, before the value addresses anything.  One check per problem and index, wave-uniform.
+// (The round-5 illegal address -- a captured graph replayed with the workspace resets as memset
+// nodes the executor ran unordered with the solver kernels, DESIGN.md "Data layout in HBM" --
+// was a use of such a value before its reset.)
+__device__ __noinline__ void index_fault(const char* what, long long v, long long lim) {
+    printf("mpcg: %s %lld outside [0, %lld) (block %d)\n", what, v, lim, (int)blockIdx.x);
+    __builtin_trap();
+}
+__device__ __forceinline__ void check_index(const char* what, int64_t v, int64_t lim) {
+    if (__builtin_expect(v < 0 || v >= lim, 0)) index_fault(what, (long long)v, (long long)lim);
+}
+// (the batch kernel: the same test without the report -- a printf call site costs the solver's
+// register allocation 11 SGPR spill slots; the trap still stops the wavefront before the access)
+__device__ __forceinline__ void check_index_quiet(int64_t v, int64_t lim) {
+    if (__builtin_expect(v < 0 || v >= lim, 0)) __builtin_trap();
+}
+
 // the wavefront's end in k_solve_wide (after its results / its parked state are written).
 // No fence: the count only tells the resume workers when every workgroup has finished, and
 // a parking workgroup has released its entry (agent scope) before it counts itself.
@@ -140,6 +161,7 @@ template <int MODEL, bool SPLIT, class T, int NB, bool DEFOPT, bool WARM>
 __device__ __forceinline__ void solve_body(const WideArgs& a) {
     if ((int64_t)blockIdx.x >= a.B) return;
     const int64_t p = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
+    check_index_quiet(p, a.n_prob);
     const int t = threadIdx.x;
     IpmProblem<T> pr;
 #pragma unroll
@@ -151,12 +173,8 @@ __device__ __forceinline__ void solve_body(const WideArgs& a) {
     IpmParams Pk = a.P;
     if constexpr (DEFOPT) ipopt_default_options(Pk);
     if (blockIdx.x == 0 && t == 0) atomicExch(a.started, 1);
-    int slot = claim_slot(a.slot_flags, a.nslots, a.nxcc, (int64_t)blockIdx.x);
-#ifdef MPCG_DEBUG_GUARD
-    if (t == 0 && (a.B <= 4 || slot < 0 || slot >= a.nslots))
-        printf("solve blk %d p %ld slot %d nslots %d xcc %d\n", (int)blockIdx.x, (long)p, slot, a.nslots, xcc_id(a.nxcc));
-    if (slot < 0 || slot >= a.nslots) slot = 0;
-#endif
+    const int slot = claim_slot(a.slot_flags, a.nslots, a.nxcc, (int64_t)blockIdx.x);
+    check_index_quiet(slot, a.nslots);
     typedef WideSolver<DevWave, MODEL, SPLIT, T, NB> Solver;
     Solver S(Pk, pr, wv, (T*)a.slots + (int64_t)slot * a.slot_elems);
     if constexpr (WARM) {
@@ -184,7 +202,8 @@ __device__ __forceinline__ void solve_body(const WideArgs& a) {
         if (t == 0) e = atomicAdd(a.park_count, 1);
         e = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
         if (e < a.park_cap) {
-            S.park((T*)a.park + (int64_t)e * a.park_stride);
+            check_index_quiet(e, a.park_cap);
+            S.park((T*)a.park + (int64_t)e * a.park_stride, p);
             if (t == 0) a.park_idx[e] = p;
             // the entry is complete: its ready flag after the stores (release, device scope)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -200,6 +219,7 @@ __device__ __forceinline__ void solve_body(const WideArgs& a) {
         // entry while the batch runs -- the list starts as -1, written by the launch)
         if (t == 0) {
             const int o = atomicAdd(a.ovf_count, 1);
+            check_index_quiet(o, a.B);
             atomicExch((unsigned long long*)&a.ovf_idx[o], (unsigned long long)p);
         }
         release_slot(a.slot_flags, slot);
@@ -377,18 +397,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         if (a.phase == 0) {
             const int e = take_parked(a);
             if (e < 0) return;
+            check_index("parked entry", e, a.park_cap);
             p = a.park_idx[e];
+            check_index("parked problem", p, a.n_prob);
             ent = (T*)a.park + (int64_t)e * a.park_stride;
         } else {
             // the whole solve, in park entry ent0 + blockIdx.x (this worker's own)
             p = take_overflow(a);
-#ifdef MPCG_DEBUG_GUARD
-            if (threadIdx.x == 0)
-                printf("resume phase 1 blk %d ent0 %d p %ld B %ld ovf_count %d ovf_taken %d done %d\n", (int)blockIdx.x, a.ent0,
-                       (long)p, (long)a.B, *a.ovf_count, *a.ovf_taken, *a.done);
-            if (p >= a.B) return;
-#endif
             if (p < 0) return;
+            check_index("overflow problem", p, a.n_prob);
+            check_index("overflow worker's park entry", (int64_t)a.ent0 + blockIdx.x, a.park_cap);
             ent = (T*)a.park + (int64_t)(a.ent0 + blockIdx.x) * a.park_stride;
         }
         IpmProblem<T> pr;
@@ -400,6 +418,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         wv.t = t;
         Solver S(a.P, pr, wv, ent + Solver::PARK_SCALARS + Lw.total());
         if (a.phase == 0) {
+            if (!S.park_entry_ok(ent, p)) index_fault("parked entry's tag / counts: problem", p, a.n_prob);
             S.unpark(ent);
         } else {
             if (a.handoff && a.handoff[p * a.handoff_stride] != 0.0f)

@@ -4363,21 +4363,36 @@ struct WideSolver {
     // phase's records).
     static constexpr int PARK_SCALARS = 32;
     MPCG_HD static int park_elems(const WideLayout& L) { return PARK_SCALARS + L.total() + L.slot(); }
-    MPCG_HD void park(T* dst) {
+    // (scalar 27: the parked problem's index, written with the scalars and checked by the worker
+    // that unparks it -- park_entry_ok: an entry read before it was complete, or one left from
+    // another launch, is caught before any of its values is used as an index)
+    static constexpr int PARK_TAG = 27;
+    MPCG_HD void park(T* dst, int64_t p) {
         const int t = wv.lane();
         wv.sync();
         if (t == 0) {
-            const T v[27] = {mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, theta_min, dw_last, delta_w_used,
+            const T v[28] = {mu, tau, theta, prim_inf, ref_phi, ref_theta, sf, theta_min, dw_last, delta_w_used,
                              (T)iter, (T)nf, (T)last_rej_filter, (T)count_filter_rej, (T)n_filter_resets,
                              (T)tiny_last, (T)tiny_flag, (T)acc_counter, (T)have_acc, (T)in_wd, (T)wd_short,
-                             (T)in_soft, (T)soft_count, (T)wd_trial_iter, (T)n_fover, (T)n_resto, (T)nf_peak};
-            for (int i = 0; i < 27; ++i) dst[i] = v[i];
+                             (T)in_soft, (T)soft_count, (T)wd_trial_iter, (T)n_fover, (T)n_resto, (T)nf_peak,
+                             (T)(double)p};
+            for (int i = 0; i < 28; ++i) dst[i] = v[i];
         }
         T* img = dst + PARK_SCALARS;
         for (int e = t; e < L.total(); e += 64) img[e] = ld(e);
         T* ws = img + L.total();  // (the acceptable point and the filter's workspace entries)
         for (int e = t; e < WideLayout::WS * N; e += 64) ws[L.SP_ACC() + e] = spill[L.SP_ACC() + e];
         for (int e = t; e < 2 * WideLayout::FX; e += 64) ws[L.SP_FLT() + e] = spill[L.SP_FLT() + e];
+    }
+    // The entry of problem p as park() wrote it: its tag is p and the scalars unpark() uses as
+    // counts or indices are in range (the filter's size indexes the LDS filter and the workspace
+    // extension; a tag of a float entry is exact up to 2^24 problems, beyond which only the range
+    // checks apply).  Wave-uniform.
+    MPCG_HD bool park_entry_ok(const T* src, int64_t p) const {
+        const double tag = (double)src[PARK_TAG];
+        const bool tag_ok = sizeof(T) == 8 || p < (1 << 24) ? tag == (double)p : tag >= 0;
+        const double nf_ = (double)src[11], it = (double)src[10], nr = (double)src[25];
+        return wv.uni(tag_ok && nf_ >= 0 && nf_ <= (double)(L.cap + WideLayout::FX) && it >= 0 && nr >= 0 ? 1 : 0) != 0;
     }
     // (the solver constructed with spill = park_entry + PARK_SCALARS + total())
     MPCG_HD void unpark(const T* src) {

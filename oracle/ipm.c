@@ -39,8 +39,11 @@
  *   required_infeasibility_reduction 0.9, constr_mult_reset_threshold 0,
  *   bound_mult_reset_threshold 1000.
  *
- * Not restated (documented in DESIGN.md): Ipopt's iterative refinement of the KKT
- * solution (the dense LDL^T solve here is accurate to rounding), slack moves for
+ * Ipopt's iterative refinement of the KKT solution (PDFullSpaceSolver: min_refinement_steps,
+ * residual_ratio_max 1e-10, at most 10 steps) is restated as ora_ipm_opts.refine_steps (off by
+ * default: the dense LDL^T solve here is accurate to rounding, and the refinement changes no
+ * fixture row's status or restoration count; see solve_step).
+ * Not restated (documented in DESIGN.md): slack moves for
  * slacks below eps*min(1,mu) (AdjustedTrialSlacks: never triggered on the fixtures -- the
  * smallest margin is recorded, ora_ipm_result.min_slack_margin), and a
  * restoration phase inside the restoration phase (a failed line search of the

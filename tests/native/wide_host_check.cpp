@@ -306,8 +306,12 @@ int main() {
                 Solver S2(two ? Pd : P, pr, wv, park.data() + Solver::PARK_SCALARS + L.total());
                 const bool parked = S0.status == Solver::NEED_RESTO;
                 if (parked) {
-                    S0.park(park.data());
+                    S0.park(park.data(), b);
                     wv.sync();
+                    if (!S2.park_entry_ok(park.data(), b)) {
+                        std::fprintf(stderr, "park entry check failed (problem %ld)\n", b);
+                        std::abort();
+                    }
                     S2.unpark(park.data());
                     S2.finish_resto();
                 }
