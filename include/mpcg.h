@@ -119,7 +119,11 @@ typedef struct mpcg_params {
      * fp64 phase's; iters counts both phases' iterations for a continued row, the fp64 solve's
      * for a row solved from the start.  Batches of more than 2,048 (solved in expected-longest-
      * first order): the B / 1024 problems ranked longest are solved by the fp64 solver from the
-     * start (diag[:, 2] = 3) while the fp32 phase runs the others. */
+     * start (diag[:, 2] = 3) while the fp32 phase runs the others.  Which rows form this head
+     * depends on the batch (its size and the other rows' ranks), so re-batching or sharding the
+     * same problems can move a row between the head (the fp64 solve from the start) and the fp32
+     * path (the fp64 continuation of its fp32 iterate); every other row's result, and every
+     * result of the fp64 configuration, is independent of the batch. */
     int32_t precision;
     /* 0 (default): Ipopt's feasibility-restoration phase where the line search fails (fp32:
      * the two phases above); 1: stop there with RESTORATION_FAILURE (9) instead, and for

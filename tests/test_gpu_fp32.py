@@ -292,12 +292,26 @@ def test_fp32_repeated_solves_on_the_default_stream(torch_cuda):
         np.testing.assert_array_equal(u0.cpu().numpy(), ref["u0"])
 
 
+def _head_rows(cf, B):
+    """The rows the single handle solves in its head: the first B / 1024 of the solve order
+    (descending float32 |c1| + |c2| + |c3|, stable), for B > 2,048 (mpcg_wide.hip head_count)."""
+    if B <= 2048:
+        return np.zeros(0, dtype=np.int64)
+    key = np.abs(cf[:B, 1:]).sum(1).astype(np.float32)
+    return np.argsort(-key, kind="stable")[:B // 1024]
+
+
 def test_fp32_multi_context_matches_single(torch_cuda):
     """The fp32 configuration through the persistent multi-GPU context (each GPU's handle solves
-    its shard on its own stream: the head forks from that stream) equals the single-handle solve
-    bitwise, with and without the head (B = 4,096 and 2,048)."""
+    its shard on its own stream: the head forks from that stream) against the single-handle solve
+    (B = 4,096 and 2,048).  One GPU: bitwise, head included.  Several GPUs: each shard has its own
+    head (none below 2,049 problems), so a row can be in one solve's head and on the other's fp32
+    path (include/mpcg.h precision): every row outside both heads bitwise, the others the same
+    status and within 1e-4 in u0 (two fp64 solves of the same NLP, from the start and from the fp32
+    iterate)."""
     torch = torch_cuda
     from mpc_ros_amd import infinity, params
+    from mpc_ros_amd.dist import shard
     from mpc_ros_amd.solver import BatchSolver, MultiSolver
 
     P = dict(params.PLUGIN_DEFAULTS, STEPS=40)
@@ -308,6 +322,14 @@ def test_fp32_multi_context_matches_single(torch_cuda):
     for B in (4096, 2048):
         r = m.solve(st[:B], cf[:B])
         ref = s.solve(st[:B], cf[:B])
+        loose = np.zeros(B, dtype=bool)
+        if len(devs) > 1:
+            loose[_head_rows(cf, B)] = True
+            for g in range(len(devs)):
+                a, n = shard(B, g, len(devs))
+                loose[a + _head_rows(cf[a:a + n], n)] = True
         for k in ("u0", "traj", "status", "iters", "obj"):
-            np.testing.assert_array_equal(r[k], ref[k])
+            np.testing.assert_array_equal(r[k][~loose], ref[k][~loose])
+        np.testing.assert_array_equal(r["status"][loose], ref["status"][loose])
+        assert np.abs(r["u0"][loose] - ref["u0"][loose]).max(initial=0.0) <= 1e-4
     m.close()
