@@ -25,7 +25,7 @@ the useful flops of SURVEY.md §8d's formula (iterations x Riccati and forward-p
 per stage, per solve) x the solves of one launch / the launch's average duration
 (HIP events on the stream it runs on), against the FP64 vector peak.  traffic =
 memory-side bytes per launch (FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3 PMC
-summary of this exact configuration (profiles/r5/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json),
+summary of this exact configuration (profiles/r6/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json),
 or null.  The line also carries hbm = algorithmic bytes per launch (B x 8 x (6 + 4 + 2 +
 3N) = B x 576 B at N = 20) / kernel time against 8 TB/s, and valu_fp64 = PMC-counted
 FP64 lane-FLOPs (redundant lanes included) / kernel time.
@@ -189,7 +189,7 @@ def latency_b1(P, st, cf, solver, dev, reps=50):
 def pmc_name(a) -> str:
     """The PMC summary of exactly this configuration (model, mode, dtype, batch, horizon)."""
     off = "_norestoration" if getattr(a, "restoration", "on") == "off" else ""
-    return a.profile_name or f"r5/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}{off}"
+    return a.profile_name or f"r6/pmc_{a.model}_{a.mode}_{a.dtype}_B{a.batch}_N{a.horizon}{off}"
 
 
 def pmc_profile(name):
@@ -428,7 +428,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64" if a.dtype == "fp64" else "f32",
+            # (the fp32 configuration's default runs an fp32 phase, then an fp64 phase on the same batch)
+            "dtype": "f64" if a.dtype == "fp64" else ("f32" if a.restoration == "off" else "f32+f64"),
             "data": "synthetic (infinity set: lemniscate course, findBestPath preprocessing; seeded per problem, "
                     + ("generated per rank on its GPU)" if a.inputs == "device" else "generated on the host)"),
             "config": {"workload": f"{'diff-drive' if a.model == 'diffdrive' else 'kinematic-bicycle'} NMPC "

@@ -3741,7 +3741,12 @@ struct WideSolver {
         T complmu = tmax(pmax - mu, mu - pmin);
         T Emu = tmax(dsd, tmax(prim_inf, complmu * iscc));
         while (wv.uni((Emu <= kappa_eps * mu || tf) && !done)) {
-            const T mnew = wv.uni_d(tmax(tmin(kappa_mu * mu, (T)pow((double)mu, (double)theta_mu)), mu_min));
+            // (mu^1.5 >= 0.2 mu exactly where sqrt(mu) >= 0.2: above 0.0401 the power -- a
+            // double-double log and exp, ~250 instructions -- cannot be the minimum, and is
+            // skipped; the first update from mu_init 0.1 is such a one)
+            const T lin_mu = kappa_mu * mu;
+            const T sup_mu = wv.uni(mu > (T)0.0401) ? lin_mu : (T)pow((double)mu, (double)theta_mu);
+            const T mnew = wv.uni_d(tmax(tmin(lin_mu, sup_mu), mu_min));
             const bool changed = mnew != mu;
             if (!changed && tf) return IPM_TINY_STEP;
             mu = mnew;

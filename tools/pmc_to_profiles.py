@@ -1,7 +1,8 @@
 """Copy the PMC summaries of a tools/gpu_r5.sh run (gpurun_out/<tag>/pmc_<cfg>/summary.json) to
-the names bench.py reads its roofline traffic from (profiles/r5/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json).
+the names bench.py reads its roofline traffic from (profiles/<round>/pmc_<model>_<mode>_<dtype>_B<B>_N<N>.json,
+round = $MPCG_PROFILE_ROUND, default r6).
 
-    python tools/pmc_to_profiles.py gpurun_out/r5"""
+    python tools/pmc_to_profiles.py gpurun_out/r6f"""
 import json
 import os
 import shutil
@@ -11,7 +12,8 @@ NAMES = {"n20": "diffdrive_solve_fp64_B65536_N20", "n40": "diffdrive_solve_fp64_
          "bic25": "bicycle_solve_fp64_B65536_N25", "n40f32": "diffdrive_solve_fp32_B65536_N40",
          "b4096": "diffdrive_solve_fp64_B4096_N20"}
 src = sys.argv[1]
-root = os.path.join(os.path.dirname(__file__), "..", "profiles", "r5")
+root = os.path.join(os.path.dirname(__file__), "..", "profiles", os.environ.get("MPCG_PROFILE_ROUND", "r6"))
+os.makedirs(root, exist_ok=True)
 for cfg, name in NAMES.items():
     f = os.path.join(src, f"pmc_{cfg}", "summary.json")
     if os.path.exists(f):
