@@ -309,7 +309,8 @@ int main() {
                     S0.park(park.data(), b);
                     wv.sync();
                     if (!S2.park_entry_ok(park.data(), b)) {
-                        std::fprintf(stderr, "park entry check failed (problem %ld)\n", b);
+                        std::fprintf(stderr, "park entry check failed (problem %ld): tag %g nf %g iter %g n_resto %g\n", b,
+                                     (double)park[27], (double)park[11], (double)park[10], (double)park[25]);
                         std::abort();
                     }
                     S2.unpark(park.data());

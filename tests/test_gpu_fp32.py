@@ -104,8 +104,9 @@ def test_fp32_full_batch_against_fp64(torch_cuda, oracle):
     other_min = np.abs(a["obj"] - b["obj"]) > 1e-6 * np.abs(b["obj"])
     print("rows in another local minimum:", np.flatnonzero(other_min).tolist(), "max |du0| elsewhere",
           du[~other_min].max())
+    # (either minimum can be the lower one: a build with another LDS layout put four rows in
+    # another minimum, one of them below fp64's -- every row still ends at a KKT point, status 1)
     assert other_min.sum() <= 4
-    assert (a["obj"][other_min] >= b["obj"][other_min] * (1 - 1e-9)).all()
     assert du[~other_min].max() <= 1e-4
     # the rows solved from the start are the fp64 solver's, bitwise
     cold = a["diag"][:, 2] == 3
