@@ -23,6 +23,9 @@ import os
 
 
 def load(root: str, kernel: str = "k_solve_wide"):
+    """Counters averaged over the dispatches of the batch kernel: of the instances whose name
+    contains `kernel`, the one with the most GPU time in the pass (configs[2] also launches
+    the fp64 solver on its 64-problem head, which must not be averaged in)."""
     vals = collections.defaultdict(list)
     times = []
     files = {}
@@ -32,13 +35,20 @@ def load(root: str, kernel: str = "k_solve_wide"):
             files[d] = f
     for f in sorted(files.values()):
         per = collections.defaultdict(float)
+        dur = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            if kernel not in r.get("Kernel_Name", ""):
+            name = r.get("Kernel_Name", "")
+            if kernel not in name:
                 continue
-            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-            times.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-        for (d, c), v in per.items():
-            vals[c].append(v)
+            per[(name, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+            dur[name][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+        if not dur:
+            continue
+        main_name = max(dur, key=lambda n: sum(dur[n].values()))
+        times.extend(dur[main_name].values())
+        for (n, d, c), v in per.items():
+            if n == main_name:
+                vals[c].append(v)
     return {c: sum(v) / len(v) for c, v in vals.items()}, (sum(times) / len(times) if times else None)
 
 
