@@ -2,8 +2,12 @@
 (diagnostic, GPU): a row that reaches it is solved by the fp64 phase from the start.  Prints, per
 limit, the launch time (HIP events, median of 5), the rows solved from the start, and the rows
 whose objective differs from the fp64 solver's by more than 1e-6 relative (another local minimum).
+With a diagnostic build (MPCG_EXTRA_CFLAGS=-DMPCG_HEAD_ENV) and HEAD_DIVS=1024,256,..., each limit
+is also run with the head (the rows solved in fp64 from the start while the fp32 phase runs) at
+B / div.
 
-    python tools/fp32_maxiter_probe.py [limits, e.g. 300,100,80,60]"""
+    [HEAD_DIVS=1024,256] python tools/fp32_maxiter_probe.py [limits, e.g. 300,100,80,60]"""
+import os
 import sys
 
 import numpy as np
@@ -32,7 +36,10 @@ def main():
     ref.solve_device(st, cf, u0, status=status, obj=obj, diag=diag)
     torch.cuda.synchronize()
     o64, u64 = obj.cpu().numpy(), u0.cpu().numpy()
-    for lim in limits:
+    divs = [d for d in os.environ.get("HEAD_DIVS", "").split(",") if d] or [None]
+    for div, lim in [(d, m) for d in divs for m in limits]:
+        if div is not None:
+            os.environ["MPCG_HEAD_DIV"] = div  # (read by the library at each solve and reserve)
         s = BatchSolver(0, P, dtype="fp32", max_iter=lim)
         s.reserve(B)
         ts = []
@@ -47,7 +54,7 @@ def main():
         o, u, dg = obj.cpu().numpy(), u0.cpu().numpy(), diag.cpu().numpy()
         om = np.flatnonzero(np.abs(o - o64) > 1e-6 * np.abs(o64))
         du = np.abs(u - u64).max(1)
-        print(f"max_iter {lim}: {np.median(ts):.2f} ms, from start {int((dg[:, 2] == 3).sum())}, continued "
+        print(f"head B/{div or 1024}, max_iter {lim}: {np.median(ts):.2f} ms, from start {int((dg[:, 2] == 3).sum())}, continued "
               f"{int((dg[:, 2] == 4).sum())}, other minima {om.tolist()}, max |du0| {du.max():.2e}, "
               f"status {np.unique(status.cpu().numpy()).tolist()}", flush=True)
         s.close()
