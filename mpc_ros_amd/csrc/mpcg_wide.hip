@@ -105,7 +105,8 @@ static IpmParams fp64_params(const IpmParams& P) {
 
 // the resume kernel of a solve kernel's instance (the general-options instance also for the
 // default-options one: the two compute bitwise the same); for the fp32 solver the fp64
-// instance of the same horizon (its escalations)
+// instance of the same horizon (a precision-1 launch parks nothing -- the fp32 phase hands every
+// ending to the fp64 phase, no_restoration = 1 keeps it -- so its workers find nothing and exit)
 static const void* resume_kernel(const IpmParams& P) {
     const bool split = P.N <= 32;
     const int nb = P.N > 64 ? 2 : 1;

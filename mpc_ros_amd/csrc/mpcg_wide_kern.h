@@ -333,12 +333,12 @@ __device__ __forceinline__ int take_parked(const WideArgs& a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return r;
 }
-// phase 1: the next problem of the overflow list, -1 when none is left.  The list may still
-// grow while the batch kernel runs (the fp32 solver's escalations are taken concurrently): an
-// entry is taken by a CAS on the taken count, its index awaited until the batch kernel has
-// published it; the worker exits once every workgroup of the batch has finished and every
-// entry is taken (or, as take_parked, when the batch kernel has not started within ~2 ms or
-// makes no progress for 20 s).
+// phase 1: the next problem of the overflow list, -1 when none is left.  The overflow launch
+// runs after the batch kernel, so the list is complete then; the protocol would also serve a
+// list that grows while the batch kernel runs: an entry is taken by a CAS on the taken count,
+// its index awaited until the batch kernel has published it; the worker exits once every
+// workgroup of the batch has finished and every entry is taken (or, as take_parked, when the
+// batch kernel has not started within ~2 ms or makes no progress for 20 s).
 __device__ __forceinline__ int64_t take_overflow(const WideArgs& a) {
     int64_t p = -1;
     if (threadIdx.x == 0) {
