@@ -80,6 +80,9 @@ def main():
             for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
                 if k in c:
                     out[k.lower() + "_frac"] = c[k] / wc
+    if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+        # (the guide: BANK_CONFLICT = the extra LDS cycles, IDX_ACTIVE = all LDS-array cycles)
+        out["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
     if "GRBM_GUI_ACTIVE" in c and t:
         out["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
     if "SQ_INSTS_VALU_FLOPS_FP64" in c:
