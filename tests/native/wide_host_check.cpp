@@ -176,6 +176,10 @@ struct HostWave {
     void sched_fence() const {}
     template <class U>
     void ld2(int i, U& a, U& b) const {
+        if (i & 1) {  // (the device's pair load is a 16-byte (fp32: 8-byte) aligned access)
+            std::fprintf(stderr, "ld2 at odd index %d\n", i);
+            std::abort();
+        }
         a = Sp<U>()[i];
         b = Sp<U>()[i + 1];
     }
