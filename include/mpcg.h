@@ -21,6 +21,14 @@
  * budget below).  As in the reference (mpc_planner.cpp:378, the status is computed and
  * then ignored), the last iterate is always returned.
  *
+ * Device-side checks: every index a kernel reads from device memory (the solve order, the
+ * workspace's slot and park-area counters and lists, a parked entry's problem tag) is
+ * range-checked before use.  A value out of range -- a workspace corrupted or reused by
+ * concurrent work outside stream order -- stops the kernel with a trap (the resume and
+ * bookkeeping kernels print the value and its bound first); the stream then reports a HIP
+ * error (a later call returns -2) and, as after any device fault, the process's HIP context
+ * is unusable.
+ *
  * Threading: one handle per thread; mpcg_set_params must not run concurrently with
  * a solve on the same handle (the reference has an unsynchronised writer here,
  * SURVEY.md §3.3 -- this API makes the ordering the caller's explicit job).  A handle's
