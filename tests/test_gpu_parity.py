@@ -287,6 +287,18 @@ def test_bicycle_matches_oracle(torch_cuda, bicycle_golden):
     check_against(s.solve(g["state"], g["coeffs"]), g)
 
 
+@pytest.mark.parametrize("N", [32, 33, 40, 80])
+def test_bicycle_horizons_against_oracle(torch_cuda, oracle, N):
+    """The bicycle model through each of its instance shapes -- the split sweeps (N = 32), the
+    unsplit ones (33, and 40: the bicycle's long-horizon bench line) and two stage blocks (80) --
+    against the oracle's bicycle restatement on problems outside the fixtures."""
+    from mpc_ros_amd import infinity, params
+
+    P = dict(params.PLUGIN_DEFAULTS, STEPS=N, MODEL=1, LF=0.5, ANGVEL=0.5)
+    st, cf = infinity.make_problems(np.arange(9700, 9708))
+    check_against(solver_for(P).solve(st, cf), oracle_ref(oracle, P, st, cf), min_same_iters=1.0)
+
+
 @pytest.mark.parametrize("N", [65, 128])
 def test_two_block_horizons(torch_cuda, oracle, N):
     """64 < STEPS <= 128: lane t carries stages t and 64 + t (the smallest and the largest
